@@ -1,0 +1,244 @@
+"""bench.py - BASELINE.json metric on MI355X:
+   queries/s (embed+top-k, k=5, b=256) over 1M x 768 corpus; p50 single-query ms
+
+One step = one batch of 256 synthetic queries (L = 32 token ids, resident in HBM)
+through the 12-layer HIP BERT encoder (K1..K7) and the exact fp32 flat search (K9+K10)
+over the corpus (BASELINE config 3; config 2/4 via --corpus-rows / --batch).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+the 1M-row corpus is row-sharded over the N ranks; each rank embeds its
+own 256 queries (DP), the ranks all-gather query embeddings (RCCL), every rank scans its
+shard for all 256*N queries, one RCCL all-gather of per-shard (score, id) candidates,
+then a device merge of each rank's own queries.  Per-GPU work is fixed as N grows
+(256 encodes + 256 x 1M scored rows): "scaling": "weak"; value = 256*N*steps / time.
+
+Rank 0 prints ONE JSON line (plus a roofline object for the dominant kernel and the
+CPU baseline - the oracle restatement timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "mediquery-rag_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from mediquery_hip import synth  # noqa: E402
+from mediquery_hip.config import DMETA_BASE  # noqa: E402
+from mediquery_hip.distributed import ShardedSearcher, shard_bounds  # noqa: E402
+from mediquery_hip.native import Encoder, FlatIndex  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--corpus-rows", type=int, default=1_000_000)
+    p.add_argument("--batch", type=int, default=256, help="queries per GPU per step")
+    p.add_argument("--seq-len", type=int, default=32)
+    p.add_argument("--k", type=int, default=5)
+    p.add_argument("--layers", type=int, default=DMETA_BASE.layers)
+    p.add_argument("--single-iters", type=int, default=50, help="single-query latency samples")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    return p.parse_args()
+
+
+def encoder_flops(cfg, B, L):
+    return B * cfg.flops_per_sequence(L)
+
+
+def cpu_baseline(args, cfg, corpus_host_fn):
+    """Oracle (torch-CPU restatement) timed on this host: encoder on 2 batches of
+    `batch` queries + fp32 mm/topk over the full corpus for 1 batch."""
+    from oracle.encoder import OracleEncoder
+    from oracle.flat import search_fp32_torch
+    from mediquery_hip.weights import synthetic_state_dict
+    threads = args.cpu_threads or os.cpu_count()
+    torch.set_num_threads(threads)
+    enc = OracleEncoder(cfg, synthetic_state_dict(cfg, 0))
+    ids, mask = synth.token_batch(args.batch, args.seq_len)
+    enc.embed(ids[:8], mask[:8])  # warm-up
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        q = enc.embed(ids, mask)
+    t_enc = (time.perf_counter() - t0) / reps
+    c = corpus_host_fn()
+    search_fp32_torch(q[:4], c[:1000], args.k, threads)  # warm-up
+    t0 = time.perf_counter()
+    search_fp32_torch(q, c, args.k, threads)
+    t_search = time.perf_counter() - t0
+    return {"value": round(args.batch / (t_enc + t_search), 2), "unit": "queries/s",
+            "cores": threads, "kind": "port",
+            "sample": ("oracle torch-CPU fp32: %d x %d-layer BERT encodes of %d queries (L=%d) "
+                       "+ 1 fp32 mm+topk of %d queries over %d x 768 rows; enc %.3f s/batch, "
+                       "search %.3f s/batch" % (reps, cfg.layers, args.batch, args.seq_len,
+                                                args.batch, c.shape[0], t_enc, t_search))}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = DMETA_BASE if args.layers == DMETA_BASE.layers else \
+        type(DMETA_BASE)(layers=args.layers)
+    B, L, K = args.batch, args.seq_len, args.k
+
+    # ---- resident inputs: corpus shard, token ids, encoder weights ------------------
+    off, cnt = shard_bounds(args.corpus_rows, world, rank)
+    full = synth.corpus_device(args.corpus_rows, 768, dev)  # same seed on every rank
+    index = FlatIndex(dim=768, capacity=cnt, device=local)
+    index.add_device(full[off:off + cnt].contiguous())
+    enc = Encoder(cfg, device=local)
+    ids_np, mask_np = synth.token_batch(B, L, seed=synth.TOKEN_SEED + rank)
+    ids = torch.from_numpy(ids_np).to(dev)
+    mask = torch.from_numpy(mask_np).to(dev)
+    q = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    nq_all = B * world
+    s_loc = torch.empty((nq_all, K), dtype=torch.float32, device=dev)
+    i_loc = torch.empty((nq_all, K), dtype=torch.int64, device=dev)
+
+    def local_search(queries, k):
+        index.search_device(queries, k, s_loc[:queries.shape[0]], i_loc[:queries.shape[0]])
+        return s_loc[:queries.shape[0]], i_loc[:queries.shape[0]]
+
+    searcher = ShardedSearcher(local_search, off)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        enc.embed_device(ids, mask, q)
+        if ev:
+            ev[1].record()
+        if world > 1:
+            s, i = searcher.search_local_batch(q, K)
+        else:
+            s, i = local_search(q, K)
+        if ev:
+            ev[2].record()
+        return s, i
+
+    # parity guard at full size: planted queries find their rows (property check)
+    pq, planted = synth.queries_device(64, full)
+    pq_s, pq_i = (searcher.search(pq, K) if world > 1 else local_search(pq, K))
+    ok_planted = bool((pq_i[:32, 0] == planted[:32]).all())
+    del full
+    torch.cuda.empty_cache()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        step(evs[it])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    t_enc = [e[0].elapsed_time(e[1]) for e in evs]
+    t_srch = [e[1].elapsed_time(e[2]) for e in evs]
+
+    # ---- single-query latency (embed 1 query + search the shard) ------------------
+    lat = []
+    if world == 1 and args.single_iters > 0:
+        ids1, mask1, q1 = ids[:1].contiguous(), mask[:1].contiguous(), q[:1]
+        for it in range(args.single_iters + 5):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            enc.embed_device(ids1, mask1, q1)
+            local_search(q1, K)
+            torch.cuda.synchronize()
+            if it >= 5:
+                lat.append((time.perf_counter() - a) * 1e3)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = nq_all * args.steps / elapsed
+    enc_ms = statistics.mean(t_enc)
+    srch_ms = statistics.mean(t_srch)
+    # algorithmic work per launch
+    enc_tflops = encoder_flops(cfg, B, L) / (enc_ms * 1e-3) / 1e12
+    rows_scanned = cnt
+    srch_flops = 2.0 * nq_all * rows_scanned * 768
+    srch_bytes = rows_scanned * 768 * 4 + nq_all * 768 * 4 + nq_all * K * 12
+    srch_tflops = srch_flops / (srch_ms * 1e-3) / 1e12
+    srch_gbs = srch_bytes / (srch_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("flat_search_kernel_bytes_per_launch")
+        except Exception:
+            traffic = None
+    enc_roof = {"kernel": "encoder forward (K1-K7, %d launches)" % (2 + 7 * cfg.layers),
+                "bound": "mfma", "achieved": round(enc_tflops, 2), "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(enc_tflops / FP32_PEAK_TFLOPS, 4),
+                "traffic": None, "ms": round(enc_ms, 3)}
+    srch_roof = {"kernel": "flat_search_kernel + merge_kernel (K9+K10)", "bound": "mfma",
+                 "achieved": round(srch_tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(srch_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                 "ms": round(srch_ms, 3), "hbm_gbs": round(srch_gbs, 1),
+                 "hbm_frac": round(srch_gbs / HBM_PEAK_GBS, 4)}
+    dominant, other = (enc_roof, srch_roof) if enc_ms >= srch_ms else (srch_roof, enc_roof)
+
+    out = {
+        "metric": "queries/s (embed+top-k, k=5, b=256) over 1M×768 corpus; p50 single-query ms",
+        "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded corpus on device, seeded token ids, seeded BERT-base weights)",
+        "config": {"workload": "BASELINE config 3: %d x 768 fp32 corpus, batch %d/GPU (L=%d) "
+                               "embed + exact top-%d" % (args.corpus_rows, B, L, K),
+                   "corpus_rows": args.corpus_rows, "rows_per_gpu": cnt, "batch_per_gpu": B,
+                   "global_batch": nq_all, "seq_len": L, "k": K,
+                   "encoder": "BERT-base %dL (dmeta-embedding-zh shape)" % cfg.layers,
+                   "parallelism": "row-shard x%d + DP encoder" % world if world > 1 else "single GPU"},
+        "p50_single_query_ms": round(statistics.median(lat), 3) if lat else None,
+        "planted_top1_ok": ok_planted,
+        "roofline": dominant,
+        "roofline_other": other,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        def corpus_host():
+            return torch.nn.functional.normalize(
+                synth.corpus_device(args.corpus_rows, 768, dev), dim=1).cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline(args, cfg, corpus_host)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out, ensure_ascii=False), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

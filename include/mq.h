@@ -1,0 +1,131 @@
+/*
+ * mq.h - C ABI of the MI355X dense-retrieval backend (libmqhip.so).
+ *
+ * Drop-in boundary for MediQuery-RAG's retrieval pair:
+ *   - the encoder replaces OllamaEmbeddings("shaw/dmeta-embedding-zh")
+ *       reference src/medical_engine.py:43, src/ingest_medical.py:104
+ *       (LangChain Embeddings.embed_query / embed_documents)
+ *   - the index replaces the Chroma collection's k-NN
+ *       reference src/medical_engine.py:52, src/ingest_medical.py:106-110,
+ *       called as vectorstore.similarity_search(query, k=5) at src/agents/nodes.py:93
+ * The reference is pure Python; its "FFI" for this path is the LangChain interface.
+ * The Python classes in mediquery-rag_amd/mediquery_hip/ bind these entry points with
+ * ctypes.
+ *
+ * Conventions
+ *   - Every entry point returns MQ_OK (0) or a negative MQ_E* status; the message of
+ *     the last failure on the calling thread is in mq_last_error().
+ *   - Pointers flagged "device" are HIP device pointers (e.g. torch data_ptr()); host
+ *     pointers are plain malloc/numpy memory.  `stream` is a hipStream_t (NULL = the
+ *     default stream).  Host-pointer calls synchronise before returning; device-pointer
+ *     calls are asynchronous on `stream`.
+ *   - Handles own their device memory; the caller owns every buffer it passes in.
+ *   - One handle is used by one thread at a time (each handle has an internal mutex).
+ *   - Row identity = insertion order (0..N-1).  Scores are cosine similarities of the
+ *     query with the L2-normalised stored row; results are ordered by score desc, then
+ *     row id asc.  k > N returns N results and pads the rest with (-inf, -1); an empty
+ *     index returns only padding.
+ */
+#ifndef MQ_H
+#define MQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQ_OK 0
+#define MQ_EINVAL -1   /* bad argument                       */
+#define MQ_ENOMEM -2   /* device or host allocation failed   */
+#define MQ_EHIP -3     /* HIP runtime error                  */
+#define MQ_EIO -4      /* file I/O error (save/load)         */
+#define MQ_ESTATE -5   /* handle in the wrong state          */
+
+#define MQ_DTYPE_F32 0
+#define MQ_DTYPE_BF16 1
+
+#define MQ_GELU_ERF 0  /* exact erf GELU (HF BERT "gelu")            */
+#define MQ_GELU_TANH 1 /* tanh approximation (ggml / llama.cpp gelu)  */
+#define MQ_POOL_CLS 0
+#define MQ_POOL_MEAN 1
+
+#define MQ_MAX_K 64    /* largest k one search call returns          */
+
+typedef struct mq_index mq_index;
+typedef struct mq_encoder mq_encoder;
+
+/* Thread-local message of the most recent failure ("" if none). */
+const char* mq_last_error(void);
+/* Library build string (arch, version). */
+const char* mq_version(void);
+/* Number of visible HIP devices (0 without a GPU); never fails. */
+int mq_device_count(void);
+
+/* ---------------------------------------------------------------- index ---- */
+/* Flat, HBM-resident index of `dim`-wide rows (dim % 32 == 0).  `capacity` rows are
+ * reserved up front (it grows on demand by re-allocation).  dtype MQ_DTYPE_F32 is the
+ * exact path; MQ_DTYPE_BF16 stores rows in bf16 (coarse path). */
+int mq_index_create(int device, int dim, int64_t capacity, int dtype, mq_index** out);
+int mq_index_destroy(mq_index* ix);
+int mq_index_size(const mq_index* ix, int64_t* n_rows);
+int mq_index_dim(const mq_index* ix, int* dim);
+/* Append n rows (K8): each row is L2-normalised on the device and stored at the next
+ * row ids.  `rows` is [n, dim] f32, host or device. */
+int mq_index_add(mq_index* ix, const float* rows, int64_t n, int rows_on_device, void* stream);
+/* Drop every row (capacity kept). */
+int mq_index_reset(mq_index* ix);
+/* Exact top-k (K9 fused score + per-block top-k, K10 merge).
+ * queries [nq, dim] f32; out_scores [nq, k] f32; out_ids [nq, k] int64.
+ * All three host (io_on_device = 0) or all device (io_on_device = 1). 1 <= k <= MQ_MAX_K. */
+int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
+                    float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
+/* Copy stored (normalised) rows [row0, row0 + n) into out [n, dim] f32 (host or device). */
+int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device, void* stream);
+/* Device pointer of the row slab ([capacity, dim] of the index dtype). */
+int mq_index_data(mq_index* ix, void** device_rows);
+/* Persistence: a flat binary slab (header + rows), see DESIGN.md. */
+int mq_index_save(mq_index* ix, const char* path);
+int mq_index_load(mq_index* ix, const char* path);
+
+/* Host-side k-way merge of per-shard candidate lists (the step after the RCCL
+ * all-gather).  scores/ids are [n_lists, nq, k_in] (list-major, as an
+ * all-gather stacks them); output [nq, k_out] by (score desc, id asc); ids < 0 are
+ * padding.  Pure CPU, no device needed. */
+int mq_topk_merge_host(const float* scores, const int64_t* ids, int n_lists, int64_t nq,
+                       int k_in, int k_out, float* out_scores, int64_t* out_ids);
+/* Same merge on the device (inputs/outputs device pointers, async on stream). */
+int mq_topk_merge_device(const float* scores, const int64_t* ids, int n_lists, int64_t nq,
+                         int k_in, int k_out, float* out_scores, int64_t* out_ids, void* stream);
+
+/* -------------------------------------------------------------- encoder ---- */
+typedef struct mq_bert_config {
+  int vocab_size;     /* 21128 */
+  int hidden;         /* 768   */
+  int layers;         /* 12    */
+  int heads;          /* 12    */
+  int ffn;            /* 3072  */
+  int max_positions;  /* 1024  */
+  int type_vocab;     /* 2     */
+  float ln_eps;       /* 1e-12 */
+  int gelu;           /* MQ_GELU_* */
+  int pooling;        /* MQ_POOL_* */
+} mq_bert_config;
+
+int mq_encoder_create(int device, const mq_bert_config* cfg, mq_encoder** out);
+int mq_encoder_destroy(mq_encoder* enc);
+/* Number of f32 values the weight blob must hold (layout: DESIGN.md / weights.py). */
+int64_t mq_encoder_weight_count(const mq_bert_config* cfg);
+/* Upload the fp32 weight blob (host pointer, n_floats values). */
+int mq_encoder_load_weights(mq_encoder* enc, const float* blob, int64_t n_floats);
+/* Compute dtype of the GEMMs: MQ_DTYPE_F32 (exact fp32 MFMA, default) or MQ_DTYPE_BF16. */
+int mq_encoder_set_precision(mq_encoder* enc, int dtype);
+/* Forward: ids/mask [B, L] int32 -> out [B, hidden] f32, unit-norm (K1..K7).
+ * All host (io_on_device = 0) or all device (io_on_device = 1).  L <= max_positions. */
+int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, int B, int L,
+                     float* out, int io_on_device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQ_H */

@@ -1,0 +1,127 @@
+// gemm_f32.hpp - exact-fp32 MFMA tile core for gfx950 (v_mfma_f32_32x32x2_f32).
+//
+// Computes D[i][j] = sum_k A[i][k] * B[j][k] for a BM x BN block tile, both operands
+// K-contiguous ("NT": activations/queries [M][K], weights/corpus rows [N][K]).
+//
+//  * 256 threads = 4 waves laid out WAVES_M x WAVES_N; each wave owns TM x TN MFMA
+//    tiles of 32x32 (f32x16 accumulators, 16 regs/lane each).
+//  * K is staged in BK = 32 slices through a double-buffered LDS image
+//    [rows][BK + 4] floats: rows of 144 B keep the staging ds_write_b128 and the
+//    fragment ds_read_b128 bank-conflict free (slot = 9*row + 4*h + q mod 16).
+//  * K order inside a slice is permuted so that one lane's 16 k-values are contiguous:
+//    MFMA step (q, s), lane half h (= lane >> 5) carries k = 16h + 4q + s for BOTH
+//    operands, so each lane fetches its fragment with 4 ds_read_b128 per slice
+//    instead of 16 ds_read_b32.  A dot product is order-free up to fp32 rounding, and
+//    the f32 MFMA is an exact fmaf chain (no TF32 / xf32 on gfx950).
+//  * Next-slice global loads are issued into registers before the MFMAs of the current
+//    slice and written to the other LDS buffer after them: one barrier per slice.
+#pragma once
+
+#include "common.hpp"
+
+namespace mq {
+
+constexpr int kBK = 32;
+constexpr int kLdsStride = kBK + 4;  // floats per staged row (144 B)
+
+template <int WAVES_M_, int WAVES_N_, int TM_, int TN_>
+struct F32Tile {
+  static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
+  static constexpr int WM = TM * 32, WN = TN * 32;  // wave tile
+  static constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
+  static constexpr int THREADS = WAVES_M * WAVES_N * kWave;
+  static constexpr int ROWS = BM + BN;
+  static constexpr int LOADS = ROWS * (kBK / 4) / THREADS;  // float4 per thread per slice
+  static constexpr int STAGE_FLOATS = ROWS * kLdsStride;
+  static_assert(THREADS == 256, "tile core assumes 256-thread workgroups");
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "block tile must be a multiple of 32");
+  static_assert(ROWS * (kBK / 4) % THREADS == 0, "staging must divide evenly");
+};
+
+// One K-slice of both operands, held in registers between the global load and the
+// LDS write (T14 "issue early / write late").
+template <class T>
+struct Stager {
+  floatx4 r[T::LOADS];
+
+  // A rows m0.. (valid < M), B rows n0.. (valid < N), columns k0 .. k0+31.
+  __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda, int M, int m0,
+                                       const float* __restrict__ B, int64_t ldb, int64_t N,
+                                       int64_t n0, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < T::LOADS; ++i) {
+      const int f = tid + i * T::THREADS;
+      const int row = f >> 3, ch = f & 7;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (i < T::BM / 32) {  // compile-time after unrolling: rows [32i, 32i+32) are A rows
+        const int gm = m0 + row;
+        if (gm < M) v = *reinterpret_cast<const floatx4*>(A + gm * lda + k0 + ch * 4);
+      } else {
+        const int64_t gn = n0 + (row - T::BM);
+        if (gn < N) v = *reinterpret_cast<const floatx4*>(B + gn * ldb + k0 + ch * 4);
+      }
+      r[i] = v;
+    }
+  }
+
+  __device__ __forceinline__ void store(float* stage, int tid) const {
+#pragma unroll
+    for (int i = 0; i < T::LOADS; ++i) {
+      const int f = tid + i * T::THREADS;
+      const int row = f >> 3, ch = f & 7;
+      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = r[i];
+    }
+  }
+};
+
+// MFMAs of one staged K-slice for wave (wm, wn).
+template <class T>
+__device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T::TM][T::TN],
+                                          int wm, int wn, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const float* as = stage + (wm * T::WM + r) * kLdsStride + h * 16;
+  const float* bs = stage + (T::BM + wn * T::WN + r) * kLdsStride + h * 16;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    floatx4 a[T::TM], b[T::TN];
+#pragma unroll
+    for (int tm = 0; tm < T::TM; ++tm)
+      a[tm] = *reinterpret_cast<const floatx4*>(as + tm * 32 * kLdsStride + q * 4);
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn)
+      b[tn] = *reinterpret_cast<const floatx4*>(bs + tn * 32 * kLdsStride + q * 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn)
+          acc[tm][tn] =
+              __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm][s], b[tn][s], acc[tm][tn], 0, 0, 0);
+  }
+}
+
+template <class T>
+__device__ __forceinline__ void zero_acc(floatx16 (&acc)[T::TM][T::TN]) {
+#pragma unroll
+  for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+}
+
+// Row (within the wave tile) of accumulator register e for this lane; the column is
+// tn * 32 + (lane & 31).  C/D map of the 32x32 MFMA family on gfx950.
+__device__ __forceinline__ int acc_row(int tm, int e, int lane) {
+  return tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5): consecutive logical tiles
+// land on the same XCD (blocks b and b+8 share one), for L2 reuse of shared panels.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+}  // namespace mq

@@ -1,0 +1,714 @@
+// index.hip - HBM-resident flat index: K8 add/normalise, K9 fused score + top-k,
+// K10 candidate merge, and the mq_index_* / mq_topk_merge_* C ABI (include/mq.h).
+//
+// Replaces the k-NN half of Chroma's similarity_search (reference
+// src/agents/nodes.py:93 on the store of src/medical_engine.py:52): exact cosine
+// ranking over L2-normalised rows, (score desc, row asc).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <vector>
+
+#include "common.hpp"
+#include "gemm_f32.hpp"
+
+namespace mq {
+
+// ============================================================ K8: add rows =====
+// One wave per row: sum of squares in registers, wave reduction, scaled store.
+// Row / max(||row||, 1e-12) - the F.normalize / Ollama normalisation semantics.
+__global__ __launch_bounds__(256) void add_rows_kernel(const float* __restrict__ src,
+                                                       float* __restrict__ dst, int64_t n,
+                                                       int dim) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const floatx4* s = reinterpret_cast<const floatx4*>(src + row * dim);
+  floatx4* d = reinterpret_cast<floatx4*>(dst + row * dim);
+  const int nv = dim >> 2;
+  float ss = 0.f;
+  for (int i = lane; i < nv; i += 64) {
+    floatx4 v = s[i];
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+  const float inv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
+  for (int i = lane; i < nv; i += 64) {
+    floatx4 v = s[i];
+    d[i] = v * inv;
+  }
+}
+
+// ================================================ K9: fused score + top-k ======
+// Register-resident running top-KC list per lane, kept sorted by (score desc, id asc).
+template <int KC>
+struct TopList {
+  float s[KC];
+  int id[KC];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      s[i] = -INFINITY;
+      id[i] = -1;
+    }
+  }
+  __device__ __forceinline__ bool beats_tail(float x, int xi) const {
+    return better(x, xi, s[KC - 1], id[KC - 1]);
+  }
+  // Branch-free bubble insertion with static indices (stays in VGPRs).
+  __device__ __forceinline__ void insert(float x, int xi) {
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const bool sw = better(x, xi, s[i], id[i]);
+      const float ts = s[i];
+      const int ti = id[i];
+      s[i] = sw ? x : ts;
+      id[i] = sw ? xi : ti;
+      x = sw ? ts : x;
+      xi = sw ? ti : xi;
+    }
+  }
+  __device__ __forceinline__ void pop_front() {
+#pragma unroll
+    for (int i = 0; i + 1 < KC; ++i) {
+      s[i] = s[i + 1];
+      id[i] = id[i + 1];
+    }
+    s[KC - 1] = -INFINITY;
+    id[KC - 1] = -1;
+  }
+};
+
+// Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
+using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
+using SearchNarrow = F32Tile<1, 4, 1, 2>;  // 32 queries x 256 rows per block (small batches)
+
+template <class T>
+struct SearchSmem {
+  static constexpr int SCORE_STRIDE = T::WN + 4;  // 68 floats: conflict-free row scans
+  static constexpr int SCORE_FLOATS = T::WM * SCORE_STRIDE;  // per wave
+  static constexpr int FLOATS = 2 * T::STAGE_FLOATS + 4 * SCORE_FLOATS;
+  static constexpr int LPQ = kWave / T::WM;  // lanes scanning one query row
+  static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget");
+};
+
+// Grid: nqt query tiles x G row groups (G % 8 == 0).  Block (qt, g) scans row tiles
+// g, g+G, g+2G, ... for queries [qt*BM, qt*BM + BM) and leaves, per lane, the top-k of
+// what it saw in cand[list][query][0..k) with list = (g*WAVES_N + wn)*LPQ + part.
+// Scores never leave the chip: each finished BMxBN tile goes accumulator -> per-wave
+// LDS tile -> one lane per (query, part) scans its row against its register top-k.
+template <class T, int KC>
+__global__ __launch_bounds__(256, 1) void flat_search_kernel(
+    const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
+    int G, int nqt, int k, float* __restrict__ cand_s, int* __restrict__ cand_i) {
+  using S = SearchSmem<T>;
+  __shared__ __attribute__((aligned(16))) float lds[S::FLOATS];
+  float* stage0 = lds;
+  float* stage1 = lds + T::STAGE_FLOATS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  float* score = lds + 2 * T::STAGE_FLOATS + wave * S::SCORE_FLOATS;
+
+  // blocks b and b+8 share an XCD: give the nqt query tiles of one row group to one
+  // XCD so the second read of each row tile is an L2 hit.
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int qt = slot % nqt, g = (slot / nqt) * 8 + xcd;
+  const int m0 = qt * T::BM;
+  const int64_t ntiles = (n_rows + T::BN - 1) / T::BN;
+  const int nk = dim / kBK;
+
+  const int q_local = lane % T::WM, part = lane / T::WM;
+  constexpr int COLS = T::WN / S::LPQ;  // columns of the wave tile this lane scans
+
+  TopList<KC> top;
+  top.init();
+
+  int64_t t = g;
+  if (t < ntiles) {
+    Stager<T> st;
+    st.load(Q, dim, nq, m0, C, dim, n_rows, t * T::BN, 0, tid);
+    st.store(stage0, tid);
+    __syncthreads();
+    int buf = 0;
+    floatx16 acc[T::TM][T::TN];
+    while (true) {
+      zero_acc<T>(acc);
+      for (int kt = 0; kt < nk; ++kt) {
+        // prefetch the next slice: (t, kt+1) or the first slice of the next row tile
+        const bool same = kt + 1 < nk;
+        const int64_t tn = same ? t : t + G;
+        const bool more = same || tn < ntiles;
+        if (more) st.load(Q, dim, nq, m0, C, dim, n_rows, tn * T::BN, same ? (kt + 1) * kBK : 0, tid);
+        mma_slice<T>(buf ? stage1 : stage0, acc, wm, wn, lane);
+        if (more) st.store(buf ? stage0 : stage1, tid);
+        __syncthreads();
+        buf ^= 1;
+      }
+      // ---- epilogue: wave tile -> LDS [query][row] (rows beyond n_rows = -inf)
+      const int64_t col0 = t * T::BN + wn * T::WN;
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int tn2 = 0; tn2 < T::TN; ++tn2) {
+          const int c = tn2 * 32 + (lane & 31);
+          const bool valid = col0 + c < n_rows;
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            score[acc_row(tm, e, lane) * S::SCORE_STRIDE + c] = valid ? acc[tm][tn2][e] : -INFINITY;
+        }
+      __syncthreads();
+      const float* row = score + q_local * S::SCORE_STRIDE + part * COLS;
+#pragma unroll
+      for (int c4 = 0; c4 < COLS; c4 += 4) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t col = col0 + part * COLS + c4 + e;
+          if (col < n_rows && top.beats_tail(v[e], (int)col)) top.insert(v[e], (int)col);
+        }
+      }
+      t += G;
+      if (t >= ntiles) break;
+    }
+  }
+
+  const int list = (g * T::WAVES_N + wn) * S::LPQ + part;
+  const int qg = m0 + wm * T::WM + q_local;
+  if (qg < nq) {
+    const int64_t base = ((int64_t)list * nq + qg) * k;
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+      if (i < k) {
+        cand_s[base + i] = top.s[i];
+        cand_i[base + i] = top.id[i];
+      }
+  }
+}
+
+// ======================================================= K10: merge lists ======
+// One block per query: every thread keeps a register top-KC of its strided share of
+// the n_lists*k_in candidates, then k_out rounds of a block arg-best pop the winners.
+template <int KC, typename IdIn>
+__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs,
+                                                    const IdIn* __restrict__ ci, int n_lists,
+                                                    int64_t nq, int k_in, int k_out,
+                                                    float* __restrict__ out_s,
+                                                    int64_t* __restrict__ out_i) {
+  __shared__ float red_s[4];
+  __shared__ long long red_i[4];
+  __shared__ int red_t[4];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // local lists hold int ids; shard-merge ids are int64 -> use a 64-bit twin list
+  float ls[KC];
+  long long li[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    ls[i] = -INFINITY;
+    li[i] = -1;
+  }
+  const int64_t n_items = (int64_t)n_lists * k_in;
+  for (int64_t it = tid; it < n_items; it += 256) {
+    const int64_t lst = it / k_in, kk = it % k_in;
+    const int64_t off = (lst * nq + q) * k_in + kk;
+    float x = cs[off];
+    long long xi = (long long)ci[off];
+    if (xi < 0) continue;
+    if (!better(x, xi, ls[KC - 1], li[KC - 1])) continue;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const bool sw = better(x, xi, ls[i], li[i]);
+      const float ts = ls[i];
+      const long long ti = li[i];
+      ls[i] = sw ? x : ts;
+      li[i] = sw ? xi : ti;
+      x = sw ? ts : x;
+      xi = sw ? ti : xi;
+    }
+  }
+  for (int r = 0; r < k_out; ++r) {
+    float bs = ls[0];
+    long long bi = li[0];
+    int bt = tid;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float os = __shfl_xor(bs, off);
+      const long long oi = __shfl_xor(bi, off);
+      const int ot = __shfl_xor(bt, off);
+      if (better(os, oi, bs, bi)) {
+        bs = os;
+        bi = oi;
+        bt = ot;
+      }
+    }
+    if (lane == 0) {
+      red_s[wave] = bs;
+      red_i[wave] = bi;
+      red_t[wave] = bt;
+    }
+    __syncthreads();
+    bs = red_s[0];
+    bi = red_i[0];
+    bt = red_t[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+      if (better(red_s[w], red_i[w], bs, bi)) {
+        bs = red_s[w];
+        bi = red_i[w];
+        bt = red_t[w];
+      }
+    if (tid == 0) {
+      out_s[q * k_out + r] = bi < 0 ? -INFINITY : bs;
+      out_i[q * k_out + r] = bi < 0 ? -1 : bi;
+    }
+    if (tid == bt && bi >= 0) {
+      // pop this thread's head
+#pragma unroll
+      for (int i = 0; i + 1 < KC; ++i) {
+        ls[i] = ls[i + 1];
+        li[i] = li[i + 1];
+      }
+      ls[KC - 1] = -INFINITY;
+      li[KC - 1] = -1;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace mq
+
+
+// ================================================================ host side =====
+using namespace mq;
+
+namespace {
+
+// Grow-only device workspace.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return MQ_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, need) != hipSuccess) MQ_FAIL(MQ_ENOMEM, "hipMalloc(%zu bytes) failed", need);
+    bytes = need;
+    return MQ_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+int kc_for(int k) { return k <= 8 ? 8 : (k <= 32 ? 32 : 64); }
+
+}  // namespace
+
+struct mq_index {
+  int device = 0;
+  int dim = 0;
+  int dtype = MQ_DTYPE_F32;
+  int64_t n = 0;    // rows stored
+  int64_t cap = 0;  // rows reserved
+  float* rows = nullptr;  // [cap, dim], every stored row unit-norm
+  int num_cus = 256;
+  DevBuf stage, cand_s, cand_i, out_s, out_i;
+  std::mutex mu;
+};
+
+namespace {
+
+template <class T, int KC>
+void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int nqt,
+                   float* cs, int* ci, hipStream_t s) {
+  hipLaunchKernelGGL((flat_search_kernel<T, KC>), dim3(G * nqt), dim3(256), 0, s, q, nq,
+                     ix->rows, ix->n, ix->dim, G, nqt, k, cs, ci);
+}
+
+template <int KC, typename IdIn>
+void launch_merge(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
+                  float* os, int64_t* oi, hipStream_t s) {
+  hipLaunchKernelGGL((merge_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
+                     n_lists, nq, k_in, k_out, os, oi);
+}
+
+template <typename IdIn>
+void merge_dispatch(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
+                    float* os, int64_t* oi, hipStream_t s) {
+  switch (kc_for(k_out)) {
+    case 8: launch_merge<8>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
+    case 32: launch_merge<32>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
+    default: launch_merge<64>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
+  }
+}
+
+struct SearchPlan {
+  bool wide;
+  int nqt;
+  int G;
+  int64_t n_lists;
+};
+
+SearchPlan plan_search(const mq_index* ix, int64_t nq) {
+  SearchPlan p;
+  p.wide = nq > 64;
+  const int BM = p.wide ? SearchWide::BM : SearchNarrow::BM;
+  const int BN = p.wide ? SearchWide::BN : SearchNarrow::BN;
+  const int wn = p.wide ? SearchWide::WAVES_N : SearchNarrow::WAVES_N;
+  const int lpq = p.wide ? SearchSmem<SearchWide>::LPQ : SearchSmem<SearchNarrow>::LPQ;
+  p.nqt = (int)((nq + BM - 1) / BM);
+  const int64_t ntiles = (ix->n + BN - 1) / BN;
+  // one 256-thread block per CU: G row groups per query tile, a multiple of 8
+  int64_t G = std::max<int64_t>(1, ix->num_cus / p.nqt);
+  G = std::min<int64_t>(G, ntiles);
+  p.G = (int)((G + 7) / 8 * 8);
+  p.n_lists = (int64_t)p.G * wn * lpq;
+  return p;
+}
+
+int fill_padding(float* os, int64_t* oi, int64_t count, hipStream_t s) {
+  std::vector<float> ps((size_t)count, -INFINITY);
+  std::vector<int64_t> pi((size_t)count, -1);
+  MQ_HIP(hipMemcpyAsync(os, ps.data(), ps.size() * 4, hipMemcpyHostToDevice, s));
+  MQ_HIP(hipMemcpyAsync(oi, pi.data(), pi.size() * 8, hipMemcpyHostToDevice, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+// Search with queries and outputs already in device memory (asynchronous).
+int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+                  hipStream_t s) {
+  if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
+  const SearchPlan p = plan_search(ix, nq);
+  const size_t n_cand = (size_t)p.n_lists * nq * k;
+  int rc = ix->cand_s.ensure(n_cand * sizeof(float));
+  if (rc) return rc;
+  rc = ix->cand_i.ensure(n_cand * sizeof(int));
+  if (rc) return rc;
+  float* cs = ix->cand_s.as<float>();
+  int* ci = ix->cand_i.as<int>();
+  const int kc = kc_for(k);
+#define MQ_SEARCH(T)                                                           \
+  switch (kc) {                                                                \
+    case 8: launch_search<T, 8>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break;   \
+    case 32: launch_search<T, 32>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
+    default: launch_search<T, 64>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
+  }
+  if (p.wide) {
+    MQ_SEARCH(SearchWide)
+  } else {
+    MQ_SEARCH(SearchNarrow)
+  }
+#undef MQ_SEARCH
+  MQ_HIP(hipGetLastError());
+  merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, k, k, os, oi, s);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
+  if (need_rows <= ix->cap) return MQ_OK;
+  int64_t new_cap = std::max<int64_t>(need_rows, ix->cap + ix->cap / 2);
+  new_cap = std::max<int64_t>(new_cap, 1024);
+  float* fresh = nullptr;
+  if (hipMalloc((void**)&fresh, (size_t)new_cap * ix->dim * sizeof(float)) != hipSuccess)
+    MQ_FAIL(MQ_ENOMEM, "hipMalloc of %lld rows failed", (long long)new_cap);
+  if (ix->n > 0) {
+    MQ_HIP(hipMemcpyAsync(fresh, ix->rows, (size_t)ix->n * ix->dim * sizeof(float),
+                          hipMemcpyDeviceToDevice, s));
+    MQ_HIP(hipStreamSynchronize(s));
+  }
+  if (ix->rows) MQ_HIP(hipFree(ix->rows));
+  ix->rows = fresh;
+  ix->cap = new_cap;
+  return MQ_OK;
+}
+
+constexpr char kMagic[8] = {'M', 'Q', 'F', 'L', 'A', 'T', '0', '1'};
+
+struct FileHeader {
+  char magic[8];
+  int32_t dim;
+  int32_t dtype;
+  int64_t n_rows;
+};
+
+}  // namespace
+
+extern "C" {
+
+int mq_index_create(int device, int dim, int64_t capacity, int dtype, mq_index** out) {
+  clear_error();
+  MQ_CHECK_ARG(out != nullptr, "out is NULL");
+  *out = nullptr;
+  MQ_CHECK_ARG(dim > 0 && dim % kBK == 0, "dim must be a positive multiple of %d (got %d)", kBK,
+               dim);
+  MQ_CHECK_ARG(capacity >= 0, "negative capacity");
+  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32, "only the f32 index dtype is implemented (got %d)", dtype);
+  DeviceGuard dg(device);
+  if (!dg.ok) MQ_FAIL(MQ_EHIP, "hipSetDevice(%d) failed", device);
+  auto ix = std::make_unique<mq_index>();
+  ix->device = device;
+  ix->dim = dim;
+  ix->dtype = dtype;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      cus > 0)
+    ix->num_cus = cus;
+  if (capacity > 0) {
+    int rc = reserve_rows(ix.get(), capacity, nullptr);
+    if (rc) return rc;
+  }
+  *out = ix.release();
+  return MQ_OK;
+}
+
+int mq_index_destroy(mq_index* ix) {
+  clear_error();
+  if (!ix) return MQ_OK;
+  {
+    DeviceGuard dg(ix->device);
+    if (ix->rows) (void)hipFree(ix->rows);
+    ix->stage.release();
+    ix->cand_s.release();
+    ix->cand_i.release();
+    ix->out_s.release();
+    ix->out_i.release();
+  }
+  delete ix;
+  return MQ_OK;
+}
+
+int mq_index_size(const mq_index* ix, int64_t* n_rows) {
+  clear_error();
+  MQ_CHECK_ARG(ix && n_rows, "NULL argument");
+  *n_rows = ix->n;
+  return MQ_OK;
+}
+
+int mq_index_dim(const mq_index* ix, int* dim) {
+  clear_error();
+  MQ_CHECK_ARG(ix && dim, "NULL argument");
+  *dim = ix->dim;
+  return MQ_OK;
+}
+
+int mq_index_data(mq_index* ix, void** device_rows) {
+  clear_error();
+  MQ_CHECK_ARG(ix && device_rows, "NULL argument");
+  *device_rows = ix->rows;
+  return MQ_OK;
+}
+
+int mq_index_reset(mq_index* ix) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->n = 0;
+  return MQ_OK;
+}
+
+int mq_index_add(mq_index* ix, const float* rows, int64_t n, int rows_on_device, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(n >= 0, "negative row count");
+  if (n == 0) return MQ_OK;
+  MQ_CHECK_ARG(rows, "NULL rows");
+  MQ_CHECK_ARG(ix->n + n < (int64_t)INT32_MAX, "index limited to 2^31-1 rows");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = reserve_rows(ix, ix->n + n, s);
+  if (rc) return rc;
+  const int64_t chunk =
+      rows_on_device ? n : std::max<int64_t>(1, std::min<int64_t>(n, (64ll << 20) / (ix->dim * 4)));
+  for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+    const int64_t nr = std::min(chunk, n - r0);
+    const float* src = rows + r0 * ix->dim;
+    if (!rows_on_device) {
+      rc = ix->stage.ensure((size_t)nr * ix->dim * 4);
+      if (rc) return rc;
+      MQ_HIP(hipMemcpyAsync(ix->stage.p, src, (size_t)nr * ix->dim * 4, hipMemcpyHostToDevice, s));
+      src = ix->stage.as<float>();
+    }
+    hipLaunchKernelGGL(add_rows_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, s, src,
+                       ix->rows + (ix->n + r0) * ix->dim, nr, ix->dim);
+    MQ_HIP(hipGetLastError());
+    if (!rows_on_device) MQ_HIP(hipStreamSynchronize(s));
+  }
+  ix->n += n;
+  return MQ_OK;
+}
+
+int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k, float* out_scores,
+                    int64_t* out_ids, int io_on_device, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(nq >= 0 && nq <= (1ll << 24), "query count %lld out of range", (long long)nq);
+  MQ_CHECK_ARG(k >= 1 && k <= MQ_MAX_K, "k must be in [1, %d] (got %d)", MQ_MAX_K, k);
+  if (nq == 0) return MQ_OK;
+  MQ_CHECK_ARG(queries && out_scores && out_ids, "NULL buffer");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (io_on_device) return search_device(ix, queries, nq, k, out_scores, out_ids, s);
+  int rc = ix->stage.ensure((size_t)nq * ix->dim * 4);
+  if (!rc) rc = ix->out_s.ensure((size_t)nq * k * 4);
+  if (!rc) rc = ix->out_i.ensure((size_t)nq * k * 8);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(ix->stage.p, queries, (size_t)nq * ix->dim * 4, hipMemcpyHostToDevice, s));
+  rc = search_device(ix, ix->stage.as<float>(), nq, k, ix->out_s.as<float>(),
+                     ix->out_i.as<int64_t>(), s);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(out_scores, ix->out_s.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(out_ids, ix->out_i.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device,
+                 void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(row0 >= 0 && n >= 0 && row0 + n <= ix->n, "rows [%lld, %lld) out of range (n=%lld)",
+               (long long)row0, (long long)(row0 + n), (long long)ix->n);
+  if (n == 0) return MQ_OK;
+  MQ_CHECK_ARG(out, "NULL output");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  MQ_HIP(hipMemcpyAsync(out, ix->rows + row0 * ix->dim, (size_t)n * ix->dim * 4,
+                        out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+  if (!out_on_device) MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_index_save(mq_index* ix, const char* path) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  FILE* f = fopen(path, "wb");
+  if (!f) MQ_FAIL(MQ_EIO, "cannot open %s for writing", path);
+  FileHeader h;
+  memcpy(h.magic, kMagic, 8);
+  h.dim = ix->dim;
+  h.dtype = ix->dtype;
+  h.n_rows = ix->n;
+  bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+  const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (ix->dim * 4));
+  std::vector<float> buf;
+  for (int64_t r0 = 0; ok && r0 < ix->n; r0 += chunk) {
+    const int64_t nr = std::min(chunk, ix->n - r0);
+    buf.resize((size_t)nr * ix->dim);
+    if (hipMemcpy(buf.data(), ix->rows + r0 * ix->dim, buf.size() * 4, hipMemcpyDeviceToHost) !=
+        hipSuccess) {
+      fclose(f);
+      MQ_FAIL(MQ_EHIP, "device->host copy failed while saving");
+    }
+    ok = fwrite(buf.data(), 4, buf.size(), f) == buf.size();
+  }
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) MQ_FAIL(MQ_EIO, "short write to %s", path);
+  return MQ_OK;
+}
+
+int mq_index_load(mq_index* ix, const char* path) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  FILE* f = fopen(path, "rb");
+  if (!f) MQ_FAIL(MQ_EIO, "cannot open %s", path);
+  FileHeader h;
+  if (fread(&h, sizeof(h), 1, f) != 1 || memcmp(h.magic, kMagic, 8) != 0) {
+    fclose(f);
+    MQ_FAIL(MQ_EIO, "%s is not an mq flat index file", path);
+  }
+  if (h.dim != ix->dim || h.dtype != ix->dtype || h.n_rows < 0) {
+    fclose(f);
+    MQ_FAIL(MQ_EINVAL, "%s holds dim %d dtype %d, index has dim %d dtype %d", path, h.dim, h.dtype,
+            ix->dim, ix->dtype);
+  }
+  ix->n = 0;
+  int rc = reserve_rows(ix, h.n_rows, nullptr);
+  if (rc) {
+    fclose(f);
+    return rc;
+  }
+  const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (ix->dim * 4));
+  std::vector<float> buf;
+  for (int64_t r0 = 0; r0 < h.n_rows; r0 += chunk) {
+    const int64_t nr = std::min(chunk, h.n_rows - r0);
+    buf.resize((size_t)nr * ix->dim);
+    if (fread(buf.data(), 4, buf.size(), f) != buf.size()) {
+      fclose(f);
+      MQ_FAIL(MQ_EIO, "%s is truncated", path);
+    }
+    if (hipMemcpy(ix->rows + r0 * ix->dim, buf.data(), buf.size() * 4, hipMemcpyHostToDevice) !=
+        hipSuccess) {
+      fclose(f);
+      MQ_FAIL(MQ_EHIP, "host->device copy failed while loading");
+    }
+  }
+  fclose(f);
+  ix->n = h.n_rows;  // rows were normalised before they were saved
+  return MQ_OK;
+}
+
+int mq_topk_merge_device(const float* scores, const int64_t* ids, int n_lists, int64_t nq,
+                         int k_in, int k_out, float* out_scores, int64_t* out_ids, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(n_lists >= 1 && nq >= 0 && k_in >= 1, "bad merge shape");
+  MQ_CHECK_ARG(k_out >= 1 && k_out <= MQ_MAX_K, "k_out must be in [1, %d]", MQ_MAX_K);
+  if (nq == 0) return MQ_OK;
+  MQ_CHECK_ARG(scores && ids && out_scores && out_ids, "NULL buffer");
+  merge_dispatch<int64_t>(scores, ids, n_lists, nq, k_in, k_out, out_scores, out_ids,
+                          (hipStream_t)stream);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_topk_merge_host(const float* scores, const int64_t* ids, int n_lists, int64_t nq, int k_in,
+                       int k_out, float* out_scores, int64_t* out_ids) {
+  clear_error();
+  MQ_CHECK_ARG(n_lists >= 1 && nq >= 0 && k_in >= 1 && k_out >= 1, "bad merge shape");
+  if (nq == 0) return MQ_OK;
+  MQ_CHECK_ARG(scores && ids && out_scores && out_ids, "NULL buffer");
+  auto better_h = [](float sa, int64_t ia, float sb, int64_t ib) {
+    return sa > sb || (sa == sb && (uint64_t)ia < (uint64_t)ib);
+  };
+  std::vector<std::pair<float, int64_t>> pool;
+  for (int64_t q = 0; q < nq; ++q) {
+    pool.clear();
+    for (int l = 0; l < n_lists; ++l) {
+      const int64_t base = ((int64_t)l * nq + q) * k_in;
+      for (int j = 0; j < k_in; ++j)
+        if (ids[base + j] >= 0) pool.emplace_back(scores[base + j], ids[base + j]);
+    }
+    const size_t take = std::min<size_t>(pool.size(), (size_t)k_out);
+    std::partial_sort(pool.begin(), pool.begin() + take, pool.end(),
+                      [&](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
+                        return better_h(a.first, a.second, b.first, b.second);
+                      });
+    for (int j = 0; j < k_out; ++j) {
+      const bool have = (size_t)j < take;
+      out_scores[q * k_out + j] = have ? pool[j].first : -INFINITY;
+      out_ids[q * k_out + j] = have ? pool[j].second : -1;
+    }
+  }
+  return MQ_OK;
+}
+
+}  // extern "C"

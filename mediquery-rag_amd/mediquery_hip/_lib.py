@@ -1,0 +1,127 @@
+"""ctypes binding of libmqhip.so (include/mq.h) - the reference-side FFI for this path.
+
+The library is built in-tree by `make -C mediquery-rag_amd/csrc` (or
+`__graft_entry__.build()`).  There is no CPU fallback: if the shared object is missing
+or fails to load, importing the product classes raises immediately.
+"""
+import ctypes
+import os
+
+try:  # load torch's HIP runtime first so the process has exactly one libamdhip64
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for host-only use
+    torch = None
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmqhip.so")
+
+MQ_OK = 0
+MQ_DTYPE_F32, MQ_DTYPE_BF16 = 0, 1
+MQ_GELU_ERF, MQ_GELU_TANH = 0, 1
+MQ_POOL_CLS, MQ_POOL_MEAN = 0, 1
+MQ_MAX_K = 64
+
+
+class MQError(RuntimeError):
+    """A libmqhip call returned a non-zero status."""
+
+    def __init__(self, fn, code, msg):
+        super().__init__("%s failed (status %d): %s" % (fn, code, msg))
+        self.code = code
+
+
+class BertConfigC(ctypes.Structure):
+    _fields_ = [("vocab_size", ctypes.c_int), ("hidden", ctypes.c_int), ("layers", ctypes.c_int),
+                ("heads", ctypes.c_int), ("ffn", ctypes.c_int), ("max_positions", ctypes.c_int),
+                ("type_vocab", ctypes.c_int), ("ln_eps", ctypes.c_float), ("gelu", ctypes.c_int),
+                ("pooling", ctypes.c_int)]
+
+    @classmethod
+    def from_config(cls, cfg):
+        return cls(cfg.vocab_size, cfg.hidden, cfg.layers, cfg.heads, cfg.ffn, cfg.max_positions,
+                   cfg.type_vocab, cfg.ln_eps, cfg.gelu, cfg.pooling)
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); every symbol include/mq.h declares
+SIGNATURES = {
+    "mq_last_error": (ctypes.c_char_p, []),
+    "mq_version": (ctypes.c_char_p, []),
+    "mq_device_count": (_I, []),
+    "mq_index_create": (_I, [_I, _I, _I64, _I, _PP]),
+    "mq_index_destroy": (_I, [_P]),
+    "mq_index_size": (_I, [_P, ctypes.POINTER(_I64)]),
+    "mq_index_dim": (_I, [_P, ctypes.POINTER(_I)]),
+    "mq_index_add": (_I, [_P, _P, _I64, _I, _P]),
+    "mq_index_reset": (_I, [_P]),
+    "mq_index_search": (_I, [_P, _P, _I64, _I, _P, _P, _I, _P]),
+    "mq_index_get": (_I, [_P, _I64, _I64, _P, _I, _P]),
+    "mq_index_data": (_I, [_P, _PP]),
+    "mq_index_save": (_I, [_P, ctypes.c_char_p]),
+    "mq_index_load": (_I, [_P, ctypes.c_char_p]),
+    "mq_topk_merge_host": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P]),
+    "mq_topk_merge_device": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P, _P]),
+    "mq_encoder_create": (_I, [_I, ctypes.POINTER(BertConfigC), _PP]),
+    "mq_encoder_destroy": (_I, [_P]),
+    "mq_encoder_weight_count": (_I64, [ctypes.POINTER(BertConfigC)]),
+    "mq_encoder_load_weights": (_I, [_P, _P, _I64]),
+    "mq_encoder_set_precision": (_I, [_P, _I]),
+    "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded library; raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libmqhip.so not found at %s - build it with "
+                              "`make -C mediquery-rag_amd/csrc` or __graft_entry__.build()" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(fn_name, rc):
+    if rc != MQ_OK:
+        raise MQError(fn_name, rc, lib().mq_last_error().decode("utf-8", "replace"))
+    return rc
+
+
+def call(fn_name, *args):
+    return check(fn_name, getattr(lib(), fn_name)(*args))
+
+
+def device_count():
+    return lib().mq_device_count()
+
+
+def ptr(a):
+    """Address of a numpy array / torch tensor / int as c_void_p."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def stream_handle(stream=None):
+    """hipStream_t of a torch stream (None -> torch's current stream on the device)."""
+    if stream is None:
+        if torch is None or not torch.cuda.is_available():
+            return None
+        stream = torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)

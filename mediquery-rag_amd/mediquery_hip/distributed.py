@@ -1,0 +1,71 @@
+"""Row-sharded search over the GPUs of one node (BASELINE config 4).
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Rank r owns
+a contiguous block of rows [offset_r, offset_r + n_r); global row id = offset_r + local
+id.  A search is:
+  1. (optional) all-gather of the ranks' query embeddings  -> every rank holds all queries
+  2. local exact top-k on the rank's shard                  (K9/K10 on the device)
+  3. ONE all-gather of the per-shard [nq, k] (score, id) candidates
+  4. merge to the global top-k by (score desc, global id asc)  (device K10 or host merge)
+Scoring needs no communication; the exchanged bytes are nq*k*12 per rank.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .native import merge_topk_device, merge_topk_host
+
+
+def shard_bounds(n_rows, world, rank):
+    """Contiguous near-equal row blocks: (offset, count) of `rank`."""
+    base, extra = divmod(n_rows, world)
+    off = rank * base + min(rank, extra)
+    return off, base + (1 if rank < extra else 0)
+
+
+class ShardedSearcher:
+    """`local_search(queries, k) -> (scores[nq,k] f32, local ids[nq,k] int64)` runs the
+    rank's shard (FlatIndex.search_device on a GPU); this class adds the global ids, the
+    candidate all-gather and the merge."""
+
+    def __init__(self, local_search, offset, group=None):
+        self.local_search = local_search
+        self.offset = int(offset)
+        self.group = group
+
+    def _all_gather(self, t):
+        world = dist.get_world_size(self.group)
+        t = t.contiguous()
+        out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if dist.get_backend(self.group) == "nccl":  # RCCL: one collective into one buffer
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        else:  # gloo (CPU tests)
+            dist.all_gather(list(out.unbind(0)), t, group=self.group)
+        return out
+
+    def gather_queries(self, q_local):
+        """[B, dim] per rank -> [world*B, dim] on every rank (rank-major)."""
+        g = self._all_gather(q_local)
+        return g.reshape(-1, q_local.shape[-1])
+
+    def search(self, queries, k):
+        """Global top-k of `queries` (identical on every rank) over all shards."""
+        s, i = self.local_search(queries, k)
+        i = torch.where(i >= 0, i + self.offset, i)
+        gs, gi = self._all_gather(s), self._all_gather(i)  # [world, nq, k]
+        nq = queries.shape[0]
+        if gs.is_cuda:
+            os_ = torch.empty((nq, k), dtype=torch.float32, device=gs.device)
+            oi = torch.empty((nq, k), dtype=torch.int64, device=gs.device)
+            merge_topk_device(gs, gi, k, os_, oi)
+            return os_, oi
+        os_, oi = merge_topk_host(gs.numpy(), gi.numpy(), k)
+        return torch.from_numpy(os_), torch.from_numpy(oi)
+
+    def search_local_batch(self, q_local, k):
+        """DP-encoded queries: gather every rank's batch, search all, keep own rows."""
+        world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+        allq = self.gather_queries(q_local)
+        s, i = self.search(allq, k)
+        B = q_local.shape[0]
+        return s[rank * B:(rank + 1) * B], i[rank * B:(rank + 1) * B]

@@ -1,0 +1,72 @@
+"""`HipBertEmbeddings` - drop-in for `langchain_ollama.OllamaEmbeddings` on MI355X.
+
+Reference call sites (unchanged by the swap):
+  * `OllamaEmbeddings(model="shaw/dmeta-embedding-zh")`  src/medical_engine.py:43,
+    src/ingest_medical.py:104
+  * `embed_documents(texts)` - reached through `Chroma.from_documents(...)`
+    (src/ingest_medical.py:106-110)
+  * `embed_query(text)` - reached through `vectorstore.similarity_search(q, k=5)`
+    (src/agents/nodes.py:93)
+Same contract as LangChain's Embeddings: lists of python floats, one unit-norm
+768-vector per text.  The forward runs in libmqhip.so (HIP, gfx950); nothing here
+computes embeddings on the CPU.
+"""
+import numpy as np
+
+from .compat import EmbeddingsBase
+from .config import BertConfig, DMETA_BASE
+from .native import Encoder
+from .tokenizer import CharTokenizer, WordPieceTokenizer
+from .weights import load_safetensors
+
+
+class HipBertEmbeddings(EmbeddingsBase):
+    """BERT-base CLS embeddings computed by the hand-written HIP encoder.
+
+    model:        kept for signature parity with OllamaEmbeddings (informational).
+    weights_path: local safetensors with HF BERT names; None = seeded synthetic weights
+                  (the dmeta weights are not available offline).
+    vocab_file:   local WordPiece vocab; None = the deterministic char tokenizer.
+    """
+
+    def __init__(self, model="shaw/dmeta-embedding-zh", *, weights_path=None, vocab_file=None,
+                 config: BertConfig = DMETA_BASE, seed=0, device=0, batch_size=256,
+                 max_length=512, **kwargs):
+        self.model = model
+        self.config = config
+        self.device = device
+        self.batch_size = int(batch_size)
+        self.max_length = min(int(max_length), config.max_positions)
+        weights = load_safetensors(weights_path, config) if weights_path else None
+        self.encoder = Encoder(config, weights=weights, seed=seed, device=device)
+        if vocab_file:
+            self.tokenizer = WordPieceTokenizer(vocab_file, max_length=self.max_length)
+        else:
+            self.tokenizer = CharTokenizer(config.vocab_size, max_length=self.max_length)
+
+    # ---- batched core -------------------------------------------------------------
+    def embed_array(self, texts):
+        """texts -> float32 [len(texts), hidden]; length-sorted batches cut padding."""
+        texts = list(texts)
+        out = np.empty((len(texts), self.config.hidden), dtype=np.float32)
+        if not texts:
+            return out
+        seqs = [self.tokenizer.encode(t) for t in texts]
+        order = sorted(range(len(seqs)), key=lambda i: len(seqs[i]))
+        for s in range(0, len(order), self.batch_size):
+            idx = order[s:s + self.batch_size]
+            L = max(len(seqs[i]) for i in idx)
+            ids = np.zeros((len(idx), L), dtype=np.int32)
+            mask = np.zeros((len(idx), L), dtype=np.int32)
+            for r, i in enumerate(idx):
+                ids[r, :len(seqs[i])] = seqs[i]
+                mask[r, :len(seqs[i])] = 1
+            out[idx] = self.encoder.embed(ids, mask)
+        return out
+
+    # ---- LangChain Embeddings interface ---------------------------------------------
+    def embed_documents(self, texts):
+        return self.embed_array(texts).tolist()
+
+    def embed_query(self, text):
+        return self.embed_array([text])[0].tolist()

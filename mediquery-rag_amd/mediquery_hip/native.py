@@ -1,0 +1,144 @@
+"""Thin handle classes over the C ABI: `FlatIndex` (mq_index_*) and `Encoder`
+(mq_encoder_*).  Host calls take/return numpy arrays; `*_device` calls take torch
+device tensors and run asynchronously on the given (or current) torch stream."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .config import BertConfig
+from .weights import state_dict_to_blob, synthetic_state_dict
+
+
+class FlatIndex:
+    """HBM-resident exact cosine index (K8 add, K9 fused score + top-k, K10 merge)."""
+
+    def __init__(self, dim=768, capacity=0, device=0, dtype=_lib.MQ_DTYPE_F32):
+        h = ctypes.c_void_p()
+        _lib.call("mq_index_create", device, dim, capacity, dtype, ctypes.byref(h))
+        self._h = h
+        self.dim = dim
+        self.device = device
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            try:
+                _lib.lib().mq_index_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
+    __del__ = close
+
+    def __len__(self):
+        n = ctypes.c_int64()
+        _lib.call("mq_index_size", self._h, ctypes.byref(n))
+        return n.value
+
+    def add(self, rows):
+        rows = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, self.dim)
+        _lib.call("mq_index_add", self._h, _lib.ptr(rows), rows.shape[0], 0, None)
+
+    def add_device(self, rows, stream=None):
+        assert rows.is_cuda and rows.dtype.is_floating_point and rows.is_contiguous()
+        _lib.call("mq_index_add", self._h, _lib.ptr(rows), rows.shape[0], 1,
+                  _lib.stream_handle(stream))
+
+    def reset(self):
+        _lib.call("mq_index_reset", self._h)
+
+    def search(self, queries, k):
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        scores = np.empty((q.shape[0], k), dtype=np.float32)
+        ids = np.empty((q.shape[0], k), dtype=np.int64)
+        _lib.call("mq_index_search", self._h, _lib.ptr(q), q.shape[0], k, _lib.ptr(scores),
+                  _lib.ptr(ids), 0, None)
+        return scores, ids
+
+    def search_device(self, queries, k, out_scores, out_ids, stream=None):
+        """queries [nq, dim] f32, out_scores [nq, k] f32, out_ids [nq, k] int64 (torch, device)."""
+        _lib.call("mq_index_search", self._h, _lib.ptr(queries), queries.shape[0], k,
+                  _lib.ptr(out_scores), _lib.ptr(out_ids), 1, _lib.stream_handle(stream))
+
+    def get(self, row0=0, n=None):
+        """Stored (normalised) rows [row0, row0+n) as float32 numpy."""
+        n = len(self) - row0 if n is None else n
+        out = np.empty((n, self.dim), dtype=np.float32)
+        _lib.call("mq_index_get", self._h, row0, n, _lib.ptr(out), 0, None)
+        return out
+
+    def data_ptr(self):
+        p = ctypes.c_void_p()
+        _lib.call("mq_index_data", self._h, ctypes.byref(p))
+        return p.value
+
+    def save(self, path):
+        _lib.call("mq_index_save", self._h, str(path).encode())
+
+    def load(self, path):
+        _lib.call("mq_index_load", self._h, str(path).encode())
+
+
+def merge_topk_host(scores, ids, k_out):
+    """[n_lists, nq, k_in] candidate lists -> global top-k_out (score desc, id asc)."""
+    scores = np.ascontiguousarray(scores, dtype=np.float32)
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    n_lists, nq, k_in = scores.shape
+    os_ = np.empty((nq, k_out), dtype=np.float32)
+    oi = np.empty((nq, k_out), dtype=np.int64)
+    _lib.call("mq_topk_merge_host", _lib.ptr(scores), _lib.ptr(ids), n_lists, nq, k_in, k_out,
+              _lib.ptr(os_), _lib.ptr(oi))
+    return os_, oi
+
+
+def merge_topk_device(scores, ids, k_out, out_scores, out_ids, stream=None):
+    n_lists, nq, k_in = scores.shape
+    _lib.call("mq_topk_merge_device", _lib.ptr(scores), _lib.ptr(ids), n_lists, nq, k_in, k_out,
+              _lib.ptr(out_scores), _lib.ptr(out_ids), _lib.stream_handle(stream))
+
+
+class Encoder:
+    """BERT encoder on one GPU (K1..K7).  `weights`: HF-named state dict, or None for
+    the seeded synthetic weights of `cfg` (see weights.py)."""
+
+    def __init__(self, cfg: BertConfig, weights=None, seed=0, device=0):
+        self.cfg = cfg
+        self.device = device
+        self._ccfg = _lib.BertConfigC.from_config(cfg)
+        h = ctypes.c_void_p()
+        _lib.call("mq_encoder_create", device, ctypes.byref(self._ccfg), ctypes.byref(h))
+        self._h = h
+        sd = weights if weights is not None else synthetic_state_dict(cfg, seed)
+        blob = state_dict_to_blob(cfg, sd)
+        n = _lib.lib().mq_encoder_weight_count(ctypes.byref(self._ccfg))
+        if n != blob.size:
+            raise ValueError("weight blob %d floats, library expects %d" % (blob.size, n))
+        _lib.call("mq_encoder_load_weights", self._h, _lib.ptr(blob), blob.size)
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            try:
+                _lib.lib().mq_encoder_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+
+    __del__ = close
+
+    def set_precision(self, dtype):
+        _lib.call("mq_encoder_set_precision", self._h, dtype)
+
+    def embed(self, ids, mask):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        mask = np.ascontiguousarray(mask, dtype=np.int32)
+        B, L = ids.shape
+        out = np.empty((B, self.cfg.hidden), dtype=np.float32)
+        _lib.call("mq_encoder_embed", self._h, _lib.ptr(ids), _lib.ptr(mask), B, L, _lib.ptr(out),
+                  0, None)
+        return out
+
+    def embed_device(self, ids, mask, out, stream=None):
+        """ids/mask int32 [B, L], out f32 [B, hidden] - torch device tensors."""
+        B, L = ids.shape
+        _lib.call("mq_encoder_embed", self._h, _lib.ptr(ids), _lib.ptr(mask), B, L, _lib.ptr(out),
+                  1, _lib.stream_handle(stream))

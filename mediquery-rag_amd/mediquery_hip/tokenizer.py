@@ -1,0 +1,130 @@
+"""Host tokenisers feeding the encoder's int32 id/mask buffers.
+
+In the reference, WordPiece tokenisation happens inside the Ollama server before the
+BERT forward (reference src/medical_engine.py:43).  The dmeta vocab is
+not available offline, so two tokenisers are provided:
+
+* `CharTokenizer` - the deterministic stand-in used for parity and benchmarks: one token
+  per non-space character (Chinese BERT tokenises CJK text one character per token),
+  id = 106 + crc32(char) mod (vocab - 106), framed by [CLS]=101 / [SEP]=102, [PAD]=0.
+* `WordPieceTokenizer` - BERT basic + greedy longest-match WordPiece over a LOCAL
+  vocab.txt, for use with real weights.
+"""
+import unicodedata
+import zlib
+
+import numpy as np
+
+PAD, UNK, CLS, SEP = 0, 100, 101, 102
+FIRST_FREE_ID = 106
+
+
+def _pack(seqs, max_length, pad_to=None):
+    """List of id lists -> (ids[B, L] int32, mask[B, L] int32), right padded."""
+    L = min(max((len(s) for s in seqs), default=0), max_length)
+    if pad_to is not None:
+        L = max(L, pad_to)
+    ids = np.zeros((len(seqs), L), dtype=np.int32)
+    mask = np.zeros((len(seqs), L), dtype=np.int32)
+    for i, s in enumerate(seqs):
+        s = s[:L]
+        ids[i, :len(s)] = s
+        mask[i, :len(s)] = 1
+    return ids, mask
+
+
+class CharTokenizer:
+    def __init__(self, vocab_size=21128, max_length=512):
+        self.vocab_size = vocab_size
+        self.max_length = max_length
+
+    def token_id(self, ch):
+        return FIRST_FREE_ID + zlib.crc32(ch.encode("utf-8")) % (self.vocab_size - FIRST_FREE_ID)
+
+    def encode(self, text):
+        body = [self.token_id(c) for c in text if not c.isspace()]
+        body = body[: self.max_length - 2]
+        return [CLS] + body + [SEP]
+
+    def __call__(self, texts, pad_to=None):
+        return _pack([self.encode(t) for t in texts], self.max_length, pad_to)
+
+
+class WordPieceTokenizer:
+    """Uncased-Chinese-BERT style tokenisation over a local vocab file."""
+
+    def __init__(self, vocab_file, max_length=512, lower_case=True, max_chars_per_word=100):
+        with open(vocab_file, "r", encoding="utf-8") as f:
+            self.vocab = {line.rstrip("\n"): i for i, line in enumerate(f)}
+        self.max_length = max_length
+        self.lower_case = lower_case
+        self.max_chars = max_chars_per_word
+        self.unk = self.vocab.get("[UNK]", UNK)
+        self.cls = self.vocab.get("[CLS]", CLS)
+        self.sep = self.vocab.get("[SEP]", SEP)
+
+    @staticmethod
+    def _is_cjk(cp):
+        return (0x4E00 <= cp <= 0x9FFF or 0x3400 <= cp <= 0x4DBF or 0x20000 <= cp <= 0x2A6DF
+                or 0x2A700 <= cp <= 0x2CEAF or 0xF900 <= cp <= 0xFAFF or 0x2F800 <= cp <= 0x2FA1F)
+
+    @staticmethod
+    def _is_punct(ch):
+        cp = ord(ch)
+        if 33 <= cp <= 47 or 58 <= cp <= 64 or 91 <= cp <= 96 or 123 <= cp <= 126:
+            return True
+        return unicodedata.category(ch).startswith("P")
+
+    def _basic(self, text):
+        words, cur = [], []
+
+        def flush():
+            if cur:
+                words.append("".join(cur))
+                cur.clear()
+        for ch in text:
+            cp = ord(ch)
+            if cp == 0 or cp == 0xFFFD or unicodedata.category(ch) in ("Cc", "Cf") and ch not in "\t\n\r":
+                continue
+            if ch.isspace():
+                flush()
+            elif self._is_cjk(cp) or self._is_punct(ch):
+                flush()
+                words.append(ch)
+            else:
+                cur.append(ch)
+        flush()
+        if self.lower_case:
+            out = []
+            for w in words:
+                w = unicodedata.normalize("NFD", w.lower())
+                out.append("".join(c for c in w if unicodedata.category(c) != "Mn"))
+            words = out
+        return [w for w in words if w]
+
+    def _wordpiece(self, word):
+        if len(word) > self.max_chars:
+            return [self.unk]
+        out, start = [], 0
+        while start < len(word):
+            end, hit = len(word), None
+            while start < end:
+                piece = word[start:end] if start == 0 else "##" + word[start:end]
+                if piece in self.vocab:
+                    hit = self.vocab[piece]
+                    break
+                end -= 1
+            if hit is None:
+                return [self.unk]
+            out.append(hit)
+            start = end
+        return out
+
+    def encode(self, text):
+        body = []
+        for w in self._basic(text):
+            body.extend(self._wordpiece(w))
+        return [self.cls] + body[: self.max_length - 2] + [self.sep]
+
+    def __call__(self, texts, pad_to=None):
+        return _pack([self.encode(t) for t in texts], self.max_length, pad_to)

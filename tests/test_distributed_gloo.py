@@ -1,0 +1,80 @@
+"""Row-sharded search across processes (world_size 2, gloo, CPU): the all-gather of
+per-shard candidates plus the merge must equal the single-index exact answer.  The
+per-shard local search here is the oracle; on GPUs it is the K9/K10 kernels."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N, DIM, NQ, K = 997, 64, 12, 7
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "mediquery-rag_amd"), root]
+    from mediquery_hip import synth
+    from mediquery_hip.distributed import ShardedSearcher, shard_bounds
+    from oracle.flat import search
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = synth.corpus(N, DIM, clustered=True)
+        off, cnt = shard_bounds(N, world, rank)
+        shard = c[off:off + cnt]
+
+        def local(q, k):
+            s, i = search(q.numpy(), shard, k)
+            return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(i)
+
+        ss = ShardedSearcher(local, off)
+        q, _ = synth.queries(NQ, c)
+        s, i = ss.search(torch.from_numpy(q), K)
+        # DP query path: each rank contributes half the batch
+        half = NQ // world
+        s2, i2 = ss.search_local_batch(torch.from_numpy(q[rank * half:(rank + 1) * half]), K)
+        out_q.put((rank, i.numpy(), s.numpy(), i2.numpy()))
+    except Exception as e:  # report instead of leaving the parent waiting
+        out_q.put((rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_equals_single_index():
+    from mediquery_hip import synth
+    from oracle.flat import exact_scores, check_topk
+    world = 2
+    ctx = mp.get_context("spawn")
+    q_out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q_out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q_out.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = synth.corpus(N, DIM, clustered=True)
+    q, _ = synth.queries(NQ, c)
+    ref = exact_scores(q, c)
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert not isinstance(r[1], str), r[1]
+    for rank, ids, scores, ids_dp in res:
+        assert check_topk(ids, scores, ref, K) == []
+        half = NQ // world
+        np.testing.assert_array_equal(ids_dp, ids[rank * half:(rank + 1) * half])
+    np.testing.assert_array_equal(res[0][1], res[1][1])

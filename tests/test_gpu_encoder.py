@@ -1,0 +1,81 @@
+"""GPU parity of the HIP BERT encoder (K1..K7) through the C ABI: against the
+transformers golden vectors and against the torch-CPU oracle on ragged shapes.
+Tolerance: |emb - ref| <= 1e-4 per element and cos >= 1 - 1e-5."""
+import os
+
+import numpy as np
+import pytest
+
+from mediquery_hip import _lib
+from mediquery_hip.config import BertConfig, DMETA_BASE, GELU_TANH, POOL_MEAN
+from mediquery_hip.native import Encoder
+from mediquery_hip.weights import synthetic_state_dict
+from oracle.encoder import OracleEncoder
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+def _close(got, ref):
+    np.testing.assert_allclose(got, ref, atol=ATOL, rtol=0)
+    cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
+    assert cos.min() >= 1 - 1e-5, cos.min()
+
+
+@pytest.fixture(scope="module")
+def g(golden):
+    return np.load(os.path.join(golden, "encoder_golden.npz"))
+
+
+@pytest.mark.parametrize("case,cfg", [
+    ("tiny_a", BertConfig(layers=2)),
+    ("tiny_b", BertConfig(layers=2)),
+    ("tiny_b_mean", BertConfig(layers=2, pooling=POOL_MEAN)),
+    ("tiny_tanh", BertConfig(layers=2, gelu=GELU_TANH)),
+    ("base", DMETA_BASE),
+])
+def test_golden(require_gpu, g, case, cfg):
+    src = case.replace("_mean", "")
+    enc = Encoder(cfg)
+    _close(enc.embed(g[src + "_ids"], g[src + "_mask"]), g[case + "_emb"])
+
+
+@pytest.mark.parametrize("B,L,ragged", [(1, 1, False), (1, 2, False), (3, 31, True), (5, 33, True),
+                                        (2, 64, False), (4, 65, True), (9, 130, True),
+                                        (2, 300, True), (1, 512, False), (70, 32, False)])
+def test_shapes_vs_oracle(require_gpu, B, L, ragged):
+    cfg = BertConfig(layers=2)
+    rng = np.random.default_rng(B * 1000 + L)
+    ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    if ragged:
+        for b in range(B):
+            n = int(rng.integers(1, L + 1))
+            mask[b, n:] = 0
+            ids[b, n:] = 0
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    _close(Encoder(cfg).embed(ids, mask), ref)
+
+
+def test_device_path_and_batch_invariance(require_gpu):
+    import torch
+    cfg = BertConfig(layers=2)
+    enc = Encoder(cfg)
+    rng = np.random.default_rng(5)
+    ids = rng.integers(106, cfg.vocab_size, (300, 32)).astype(np.int32)
+    mask = np.ones_like(ids)
+    host = enc.embed(ids, mask)
+    dev = torch.device("cuda", 0)
+    out = torch.empty((300, 768), dtype=torch.float32, device=dev)
+    enc.embed_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+    # a sequence's embedding does not depend on what else is in the batch
+    np.testing.assert_allclose(enc.embed(ids[7:8], mask[7:8])[0], host[7], atol=1e-6)
+
+
+def test_errors(require_gpu):
+    enc = Encoder(BertConfig(layers=1, max_positions=64))
+    with pytest.raises(_lib.MQError, match="max_positions"):
+        enc.embed(np.zeros((1, 65), np.int32), np.ones((1, 65), np.int32))
+    assert enc.embed(np.zeros((0, 8), np.int32), np.zeros((0, 8), np.int32)).shape == (0, 768)

@@ -1,0 +1,145 @@
+"""GPU parity of the flat index (K8 add, K9 fused score + top-k, K10 merge) through the
+C ABI against the float64 oracle (tie-group-aware: ids exact outside tie groups,
+cosine within 1e-4)."""
+import os
+
+import numpy as np
+import pytest
+
+from mediquery_hip import synth
+from mediquery_hip.native import FlatIndex, merge_topk_device, merge_topk_host
+from oracle.flat import check_topk, exact_scores, search
+
+pytestmark = pytest.mark.gpu
+
+
+def _index(rows):
+    ix = FlatIndex(dim=rows.shape[1])
+    ix.add(rows)
+    return ix
+
+
+def test_flat_golden_fixture(require_gpu, golden):
+    f = np.load(os.path.join(golden, "flat_golden.npz"))
+    c = synth.corpus(int(f["n"]), int(f["dim"]), clustered=True)
+    q, planted = synth.queries(int(f["nq"]), c)
+    ref = exact_scores(q, c)
+    ix = _index(c)
+    for k in (5, 50):
+        s, i = ix.search(q, k)
+        assert check_topk(i, s, ref, k) == [], k
+        pl = planted >= 0
+        assert (i[pl, 0] == planted[pl]).all()
+
+
+@pytest.mark.parametrize("n,nq,k", [
+    (1, 1, 1), (5, 3, 8), (127, 7, 5), (128, 32, 5), (129, 33, 9), (1000, 64, 32),
+    (1000, 65, 33), (4099, 128, 5), (4099, 200, 64), (3000, 256, 5), (700, 1, 64), (2500, 300, 17)])
+def test_shapes_vs_oracle(require_gpu, n, nq, k):
+    c = synth.corpus(n, 768, seed=n)
+    q, _ = synth.queries(nq, c, seed=nq)
+    ix = _index(c)
+    s, i = ix.search(q, k)
+    ref = exact_scores(q, c)
+    kk = min(k, n)
+    assert check_topk(i[:, :kk], s[:, :kk], ref, k) == []
+    if k > n:  # k > N: N results, then (-inf, -1) padding
+        assert (i[:, n:] == -1).all() and np.isneginf(s[:, n:]).all()
+
+
+def test_other_dims(require_gpu):
+    for dim in (32, 256, 1024):
+        c = synth.corpus(900, dim, seed=dim)
+        q, _ = synth.queries(20, c)
+        s, i = _index(c).search(q, 10)
+        assert check_topk(i, s, exact_scores(q, c), 10) == []
+
+
+def test_duplicates_and_exact_ties(require_gpu):
+    c = synth.corpus(300, 768)
+    c[200] = c[10]          # exact duplicate rows: ids must come out in row order
+    c[201] = 3.0 * c[10]    # same direction, different norm -> same cosine after K8
+    q = c[10:11] / np.linalg.norm(c[10])
+    s, i = _index(c).search(q, 3)
+    assert i[0].tolist() == [10, 200, 201]
+    np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
+
+
+def test_empty_append_reset_get(require_gpu, tmp_path):
+    ix = FlatIndex(dim=768)
+    q, _ = synth.queries(4, synth.corpus(10, 768))
+    s, i = ix.search(q, 5)
+    assert (i == -1).all()
+    c = synth.corpus(1000, 768)
+    ix.add(c[:300])
+    ix.add(c[300:])        # appended rows keep insertion-order ids
+    assert len(ix) == 1000
+    s, i = ix.search(q, 5)
+    assert check_topk(i, s, exact_scores(q, c), 5) == []
+    got = ix.get(295, 10)
+    np.testing.assert_allclose(got, c[295:305] / np.linalg.norm(c[295:305], axis=1, keepdims=True), atol=1e-6)
+    p = str(tmp_path / "ix.flat")
+    ix.save(p)
+    ix2 = FlatIndex(dim=768)
+    ix2.load(p)
+    s2, i2 = ix2.search(q, 5)
+    np.testing.assert_array_equal(i2, i)
+    np.testing.assert_array_equal(s2, s)
+    ix.reset()
+    assert len(ix) == 0 and (ix.search(q, 3)[1] == -1).all()
+
+
+def test_device_pointer_path_and_device_merge(require_gpu):
+    import torch
+    dev = torch.device("cuda", 0)
+    c = synth.corpus(5000, 768, clustered=True)
+    q, _ = synth.queries(96, c)
+    ix = FlatIndex(dim=768)
+    ix.add_device(torch.from_numpy(c).to(dev))
+    qd = torch.from_numpy(q).to(dev)
+    s = torch.empty((96, 10), dtype=torch.float32, device=dev)
+    i = torch.empty((96, 10), dtype=torch.int64, device=dev)
+    ix.search_device(qd, 10, s, i)
+    torch.cuda.synchronize()
+    assert check_topk(i.cpu().numpy(), s.cpu().numpy(), exact_scores(q, c), 10) == []
+    # device merge of 3 shards == host merge == single index
+    shards = [(0, 1700), (1700, 3300), (3300, 5000)]
+    ss, ii = [], []
+    for a, b in shards:
+        sub = FlatIndex(dim=768)
+        sub.add(c[a:b])
+        s_, i_ = sub.search(q, 10)
+        ss.append(s_)
+        ii.append(np.where(i_ >= 0, i_ + a, -1))
+    hs, hi = merge_topk_host(np.stack(ss), np.stack(ii), 10)
+    np.testing.assert_array_equal(hi, i.cpu().numpy())
+    ds = torch.empty_like(s)
+    di = torch.empty_like(i)
+    merge_topk_device(torch.from_numpy(np.stack(ss)).to(dev), torch.from_numpy(np.stack(ii)).to(dev), 10, ds, di)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(di.cpu().numpy(), hi)
+
+
+def test_full_size_1m_planted_and_fp64_reference(require_gpu):
+    """BASELINE config 3 size (1M x 768, B = 256, k = 5): planted queries hit their
+    rows, and the ids equal a float64 torch reference of the same device corpus."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rows = synth.corpus_device(1_000_000, 768, dev)
+    q, planted = synth.queries_device(256, rows)
+    ix = FlatIndex(dim=768, capacity=1_000_000)
+    ix.add_device(rows)
+    s = torch.empty((256, 5), dtype=torch.float32, device=dev)
+    i = torch.empty((256, 5), dtype=torch.int64, device=dev)
+    ix.search_device(q, 5, s, i)
+    torch.cuda.synchronize()
+    pl = planted >= 0
+    assert bool((i[pl, 0] == planted[pl]).all())
+    normed = torch.nn.functional.normalize(rows.double(), dim=1)
+    ref_full = q.double() @ normed.T                         # [256, 1M] float64
+    rv, ri = torch.topk(ref_full, 6, dim=1)
+    del normed
+    fails = check_topk(i.cpu().numpy(), s.cpu().numpy(), None, 5,
+                       ref_top=(rv.cpu().numpy(), ri.cpu().numpy()), n_rows=1_000_000,
+                       ref_lookup=lambda b, ids: ref_full[b, torch.as_tensor(ids, device=dev)].cpu().numpy())
+    assert fails == []

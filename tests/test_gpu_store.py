@@ -1,0 +1,77 @@
+"""The drop-in boundary driven exactly as the reference drives it (BASELINE config 1):
+  ingest  - Chroma.from_documents(documents=docs, embedding=embeddings,
+            persist_directory=DB_PATH)                       src/ingest_medical.py:106-110
+  engine  - Chroma(persist_directory=DB_PATH, embedding_function=embeddings)
+                                                              src/medical_engine.py:52
+  node    - [d.page_content for d in vectorstore.similarity_search(q, k=5)]
+                                                              src/agents/nodes.py:93-94
+with HipBertEmbeddings / HipChroma swapped in.  Expected: the committed config-1 golden
+(transformers encoder + float64 exact top-5) within tie groups."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from mediquery_hip import Document, HipBertEmbeddings, HipChroma
+from oracle.flat import check_topk, exact_scores
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def embeddings(require_gpu):
+    return HipBertEmbeddings(model="shaw/dmeta-embedding-zh")
+
+
+@pytest.fixture(scope="module")
+def docs(corpus_docs):
+    return [Document(page_content=d["page_content"], metadata=d["metadata"]) for d in corpus_docs["docs"]]
+
+
+def test_ingest_then_engine_then_retrieve(embeddings, docs, golden, tmp_path_factory):
+    db = str(tmp_path_factory.mktemp("medical_db"))
+    Cls = HipChroma
+    Cls.from_documents(documents=docs, embedding=embeddings, persist_directory=db)   # ingest
+    vectorstore = Cls(persist_directory=db, embedding_function=embeddings)           # engine
+    assert len(vectorstore) == 154
+    g = np.load(os.path.join(golden, "config1_golden.npz"))
+    queries = json.load(open(os.path.join(golden, "config1_queries.json"), encoding="utf-8"))["queries"]
+    contents = [d.page_content for d in docs]
+    # document embeddings from the GPU match the golden ones
+    d_emb = embeddings.embed_array(contents)
+    np.testing.assert_allclose(d_emb, g["doc_emb"], atol=1e-4)
+    ref = exact_scores(g["query_emb"], g["doc_emb"])
+    for qi, q in enumerate(queries):
+        got = [d.page_content for d in vectorstore.similarity_search(q, k=5)]      # retrieve node
+        assert len(got) == 5
+        rows = [r for r, _ in vectorstore._search_rows(vectorstore._embed_query(q), 5)]
+        assert [contents[r] for r in rows] == got
+        scores = [c for _, c in vectorstore._search_rows(vectorstore._embed_query(q), 5)]
+        assert check_topk([rows], [scores], ref[qi:qi + 1], 5) == [], q
+
+
+def test_scores_distance_semantics_and_edges(embeddings, docs):
+    store = HipChroma.from_documents(documents=docs[:20], embedding=embeddings)
+    res = store.similarity_search_with_score(docs[3].page_content, k=3)
+    assert res[0][0].page_content == docs[3].page_content
+    assert res[0][1] == pytest.approx(0.0, abs=1e-5)             # squared L2 of unit vectors
+    assert all(a[1] <= b[1] for a, b in zip(res, res[1:]))      # ascending distance
+    assert len(store.similarity_search("血糖", k=50)) == 20     # k > N returns N
+    empty = HipChroma(embedding_function=embeddings)
+    assert empty.similarity_search("血糖", k=5) == []
+    ids = store.add_texts(["额外的文本"], metadatas=[{"title": "extra", "tags": "t"}])
+    assert store.similarity_search("额外的文本", k=1)[0].metadata["title"] == "extra"
+    store.delete(ids)
+    assert len(store) == 20
+    f = store.similarity_search(docs[5].page_content, k=3, filter={"title": docs[7].metadata["title"]})
+    assert [d.metadata["title"] for d in f] == [docs[7].metadata["title"]]
+
+
+def test_batch_search_matches_single(embeddings, docs):
+    store = HipChroma.from_documents(documents=docs, embedding=embeddings)
+    qs = [d.page_content[:12] for d in docs[:40]]
+    batch = store.similarity_search_batch(qs, k=5)
+    for q, b in zip(qs, batch):
+        single = store.similarity_search(q, k=5)
+        assert [d.page_content for d in b] == [d.page_content for d in single]
