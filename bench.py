@@ -148,6 +148,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    enc.read_timing()
+    index.read_timing()
+    enc.set_timing(True)
+    index.set_timing(True)
     t0 = time.perf_counter()
     for it in range(args.steps):
         step(evs[it])
@@ -162,6 +166,10 @@ def main():
         elapsed = float(t.item())
     t_enc = [e[0].elapsed_time(e[1]) for e in evs]
     t_srch = [e[1].elapsed_time(e[2]) for e in evs]
+    stage_ms = {k: v / args.steps for k, v in enc.read_timing().items()}
+    stage_ms.update({k: v / args.steps for k, v in index.read_timing().items()})
+    enc.set_timing(False)
+    index.set_timing(False)
 
     # ---- single-query latency (embed 1 query + search the shard) ------------------
     lat = []
@@ -185,31 +193,44 @@ def main():
     value = nq_all * args.steps / elapsed
     enc_ms = statistics.mean(t_enc)
     srch_ms = statistics.mean(t_srch)
-    # algorithmic work per launch
-    enc_tflops = encoder_flops(cfg, B, L) / (enc_ms * 1e-3) / 1e12
-    rows_scanned = cnt
-    srch_flops = 2.0 * nq_all * rows_scanned * 768
-    srch_bytes = rows_scanned * 768 * 4 + nq_all * 768 * 4 + nq_all * K * 12
-    srch_tflops = srch_flops / (srch_ms * 1e-3) / 1e12
-    srch_gbs = srch_bytes / (srch_ms * 1e-3) / 1e9
+    H, F, NL = cfg.hidden, cfg.ffn, cfg.layers
+    M = B * L
+    full, last = NL - 1, 1  # the CLS-pooled last layer runs out-proj/FFN on B rows only
+    flops = {  # algorithmic FLOPs per step actually issued by each kernel class
+        "qkv_gemm": NL * 2.0 * M * 3 * H * H,
+        "attention": NL * 4.0 * B * L * L * H,
+        "out_proj_gemm": (full * M + last * B) * 2.0 * H * H,
+        "ffn_up_gemm": (full * M + last * B) * 2.0 * H * F,
+        "ffn_down_gemm": (full * M + last * B) * 2.0 * H * F,
+        "flat_search_kernel": 2.0 * nq_all * cnt * 768,
+    }
+    kernels = {}
+    for name, ms in stage_ms.items():
+        d = {"ms_per_step": round(ms, 4)}
+        if name in flops and ms > 0:
+            tf = flops[name] / (ms * 1e-3) / 1e12
+            d.update(tflops=round(tf, 2), frac_fp32_peak=round(tf / FP32_PEAK_TFLOPS, 4))
+        kernels[name] = d
+    # dominant kernel = the kernel class with the most device time per step
+    dom = max((n for n in flops if stage_ms.get(n, 0) > 0), key=lambda n: stage_ms[n])
+    dom_tf = flops[dom] / (stage_ms[dom] * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("flat_search_kernel_bytes_per_launch")
+            traffic = json.load(open(pmc)).get(dom)
         except Exception:
             traffic = None
-    enc_roof = {"kernel": "encoder forward (K1-K7, %d launches)" % (2 + 7 * cfg.layers),
-                "bound": "mfma", "achieved": round(enc_tflops, 2), "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(enc_tflops / FP32_PEAK_TFLOPS, 4),
-                "traffic": None, "ms": round(enc_ms, 3)}
-    srch_roof = {"kernel": "flat_search_kernel + merge_kernel (K9+K10)", "bound": "mfma",
-                 "achieved": round(srch_tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                 "frac": round(srch_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                 "ms": round(srch_ms, 3), "hbm_gbs": round(srch_gbs, 1),
-                 "hbm_frac": round(srch_gbs / HBM_PEAK_GBS, 4)}
-    dominant, other = (enc_roof, srch_roof) if enc_ms >= srch_ms else (srch_roof, enc_roof)
-
+    srch_bytes = cnt * 768 * 4 + nq_all * 768 * 4 + nq_all * K * 12
+    srch_k = stage_ms.get("flat_search_kernel", srch_ms)
+    roofline = {"kernel": dom, "bound": "mfma", "achieved": round(dom_tf, 2),
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(dom_tf / FP32_PEAK_TFLOPS, 4),
+                "traffic": traffic}
+    search_roof = {"kernel": "flat_search_kernel", "bound": "mfma",
+                   "achieved_tflops": kernels.get("flat_search_kernel", {}).get("tflops"),
+                   "hbm_gbs_algorithmic": round(srch_bytes / (srch_k * 1e-3) / 1e9, 1),
+                   "hbm_frac": round(srch_bytes / (srch_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "bytes_per_launch": srch_bytes, "flops_per_launch": flops["flat_search_kernel"]}
     out = {
         "metric": "queries/s (embed+top-k, k=5, b=256) over 1M×768 corpus; p50 single-query ms",
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
@@ -224,8 +245,10 @@ def main():
                    "parallelism": "row-shard x%d + DP encoder" % world if world > 1 else "single GPU"},
         "p50_single_query_ms": round(statistics.median(lat), 3) if lat else None,
         "planted_top1_ok": ok_planted,
-        "roofline": dominant,
-        "roofline_other": other,
+        "roofline": roofline,
+        "search_roofline": search_roof,
+        "encoder_ms": round(enc_ms, 3), "search_ms": round(srch_ms, 3),
+        "kernels": kernels,
     }
     if world == 1 and not args.no_cpu_baseline:
         def corpus_host():

@@ -84,6 +84,11 @@ int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
 int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device, void* stream);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
+/* Device-time accounting with HIP events on the launch stream (off by default).
+ * read_timing returns the ms accumulated since the last read: [0] K9 score + top-k,
+ * [1] K10 merge; it synchronises on the recorded events and resets the counters. */
+int mq_index_set_timing(mq_index* ix, int enabled);
+int mq_index_read_timing(mq_index* ix, float* ms, int n);
 /* Persistence: a flat binary slab (header + rows), see DESIGN.md. */
 int mq_index_save(mq_index* ix, const char* path);
 int mq_index_load(mq_index* ix, const char* path);
@@ -120,6 +125,13 @@ int64_t mq_encoder_weight_count(const mq_bert_config* cfg);
 int mq_encoder_load_weights(mq_encoder* enc, const float* blob, int64_t n_floats);
 /* Compute dtype of the GEMMs: MQ_DTYPE_F32 (exact fp32 MFMA, default) or MQ_DTYPE_BF16. */
 int mq_encoder_set_precision(mq_encoder* enc, int dtype);
+/* Device-time accounting per kernel class (HIP events on the launch stream, off by
+ * default).  read_timing returns ms since the last read for the stages
+ * [0] embed+LN, [1] QKV GEMM, [2] attention, [3] out-proj GEMM, [4] LayerNorm,
+ * [5] FFN-up GEMM, [6] FFN-down GEMM, [7] pool+normalise, and resets them. */
+#define MQ_ENC_STAGES 8
+int mq_encoder_set_timing(mq_encoder* enc, int enabled);
+int mq_encoder_read_timing(mq_encoder* enc, float* ms, int n);
 /* Forward: ids/mask [B, L] int32 -> out [B, hidden] f32, unit-norm (K1..K7).
  * All host (io_on_device = 0) or all device (io_on_device = 1).  L <= max_positions. */
 int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, int B, int L,

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "mq.h"
 
@@ -70,5 +71,51 @@ constexpr int kWave = 64;
 __device__ __forceinline__ bool better(float sa, int64_t ia, float sb, int64_t ib) {
   return sa > sb || (sa == sb && (unsigned long long)ia < (unsigned long long)ib);
 }
+
+// Optional per-kernel-class device timeline: one HIP event per launch boundary on the
+// launch stream; interval i (event i -> i+1) is charged to stage[i].  Off by default;
+// drain() folds the intervals into acc[] (it synchronises on the last event).
+struct Timeline {
+  static constexpr int kMaxStages = 16;
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  std::vector<int> stage;
+  size_t used = 0;
+  float acc[kMaxStages] = {};
+
+  void mark(hipStream_t st, int next_stage) {
+    if (!on) return;
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      pool.push_back(e);
+    }
+    (void)hipEventRecord(pool[used], st);
+    stage.resize(used + 1);
+    stage[used] = next_stage;
+    ++used;
+  }
+  void close(hipStream_t st) { mark(st, -1); }
+  void drain() {
+    if (used >= 2) {
+      (void)hipEventSynchronize(pool[used - 1]);
+      for (size_t i = 0; i + 1 < used; ++i) {
+        if (stage[i] < 0 || stage[i] >= kMaxStages) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pool[i], pool[i + 1]) == hipSuccess) acc[stage[i]] += ms;
+      }
+    }
+    used = 0;
+  }
+  // copy out and reset the accumulated milliseconds
+  void read(float* out, int n) {
+    drain();
+    for (int i = 0; i < n && i < kMaxStages; ++i) out[i] = acc[i];
+    for (float& a : acc) a = 0.f;
+  }
+  ~Timeline() {
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  }
+};
 
 }  // namespace mq

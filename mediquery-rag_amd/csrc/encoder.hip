@@ -39,13 +39,15 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // ------------------------------------------------------------------ GEMM -------
 // out[M,N] = epi(A[M,K] . W[N,K]^T + bias[N] (+ resid[M,N])), K % 32 == 0.
+// Row strides lda / ldr / ldo (in floats) let the CLS-only last layer run on every
+// L-th row of the activations without a gather.
 template <class T, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A,
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
-                                                         const float* __restrict__ resid,
-                                                         float* __restrict__ out, int M, int N,
-                                                         int K) {
+                                                         const float* __restrict__ resid, int ldr,
+                                                         float* __restrict__ out, int ldo, int M,
+                                                         int N, int K) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
   float* stage0 = lds;
   float* stage1 = lds + T::STAGE_FLOATS;
@@ -59,12 +61,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
   floatx16 acc[T::TM][T::TN];
   zero_acc<T>(acc);
   Stager<T> st;
-  st.load(A, K, M, m0, W, K, N, n0, 0, tid);
+  st.bind(A, lda, M, m0, W, K, N, n0, tid);
+  st.load(0);
   st.store(stage0, tid);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
-    if (more) st.load(A, K, M, m0, W, K, N, n0, (kt + 1) * kBK, tid);
+    if (more) st.load((kt + 1) * kBK);
     mma_slice<T>((kt & 1) ? stage1 : stage0, acc, wm, wn, lane);
     if (more) st.store((kt & 1) ? stage0 : stage1, tid);
     __syncthreads();
@@ -82,11 +85,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
         const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
         if (row >= M) continue;
         float v = acc[tm][tn][e] + b;
-        const int64_t o = (int64_t)row * N + col;
         if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
         if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-        if (EPI == EPI_RESID) v += resid[o];
-        out[o] = v;
+        if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+        out[(int64_t)row * ldo + col] = v;
       }
   }
 }
@@ -158,109 +160,109 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 }
 
 // ------------------------------------------------------------ K3 attention ----
-// Block = (64-query tile, head, sequence); dh = 64.  K/V tiles of 64 keys staged in
-// LDS; each of 4 lanes per query row owns 16 keys for QK^T and 16 output dims for PV.
-// Online softmax (running max / sum) in fp32; masked keys contribute exactly 0.
-constexpr int kAttQ = 64, kAttK = 64, kDh = 64;
+// One 64-thread workgroup (one wave) per (sequence, head, 32-query tile); dh = 64.
+// Scores are computed TRANSPOSED on the f32 MFMA: S^T[key][query] = K . Q^T, so keys
+// sit in the accumulator registers and queries on the lanes; the softmax over keys is
+// then 16 in-register values + one cross-half exchange per query, and S^T is already
+// the B operand of O^T[d][query] = V^T . P^T (no transpose, no LDS for P).
+// Operand k-order: lane half h carries head dims 32h..32h+31 for QK^T (one contiguous
+// 128-B read per row per lane), and key (s&3) + 8(s>>2) + 4h at PV step s (the
+// accumulator row map).  Online softmax across 32-key tiles; masked keys weigh 0.
+constexpr int kDh = 64;
 
-__global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv,
-                                                        const int* __restrict__ mask, int L,
-                                                        int H, float scale,
-                                                        float* __restrict__ ctx) {
-  __shared__ float qs[kAttQ][kDh + 1];
-  __shared__ float ks[kAttK][kDh + 1];
-  __shared__ float vs[kAttK][kDh + 4];
-  __shared__ float ps[kAttQ][kAttK + 1];
-  __shared__ int ms[kAttK];
-
-  const int q0 = blockIdx.x * kAttQ, h = blockIdx.y, bseq = blockIdx.z;
-  const int tid = threadIdx.x, qi = tid >> 2, part = tid & 3;
+__global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
+                                                       const int* __restrict__ mask, int L,
+                                                       int H, int heads, int q_tiles,
+                                                       float scale, float* __restrict__ ctx) {
+  __shared__ float obuf[32][kDh + 1];
+  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+  const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
+  const int bseq = blockIdx.x / (q_tiles * heads);
+  const int q0 = qt * 32;
   const int64_t row0 = (int64_t)bseq * L;
   const int ld = 3 * H;
 
-  // Q tile -> LDS (pre-scaled)
-  for (int e = tid; e < kAttQ * (kDh / 4); e += 256) {
-    const int r = e / (kDh / 4), c4 = e % (kDh / 4);
-    floatx4 v = {0.f, 0.f, 0.f, 0.f};
-    if (q0 + r < L)
-      v = *reinterpret_cast<const floatx4*>(qkv + (row0 + q0 + r) * ld + h * kDh + c4 * 4);
-    qs[r][c4 * 4 + 0] = v.x * scale;
-    qs[r][c4 * 4 + 1] = v.y * scale;
-    qs[r][c4 * 4 + 2] = v.z * scale;
-    qs[r][c4 * 4 + 3] = v.w * scale;
-  }
-
-  float m_run = -INFINITY, l_run = 0.f;
-  float o[16];
+  float qf[32];
+  {
+    const float* src = qkv + (row0 + min(q0 + r, L - 1)) * ld + h * kDh + hh * 32;
 #pragma unroll
-  for (int d = 0; d < 16; ++d) o[d] = 0.f;
-
-  for (int k0 = 0; k0 < L; k0 += kAttK) {
-    __syncthreads();  // previous tile fully consumed (and Q visible on the first pass)
-    for (int e = tid; e < kAttK * (kDh / 4); e += 256) {
-      const int r = e / (kDh / 4), c4 = e % (kDh / 4);
-      floatx4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
-      if (k0 + r < L) {
-        const float* base = qkv + (row0 + k0 + r) * ld + h * kDh + c4 * 4;
-        kv = *reinterpret_cast<const floatx4*>(base + H);
-        vv = *reinterpret_cast<const floatx4*>(base + 2 * H);
-      }
-      ks[r][c4 * 4 + 0] = kv.x;
-      ks[r][c4 * 4 + 1] = kv.y;
-      ks[r][c4 * 4 + 2] = kv.z;
-      ks[r][c4 * 4 + 3] = kv.w;
-      *reinterpret_cast<floatx4*>(&vs[r][c4 * 4]) = vv;
+    for (int i = 0; i < 8; ++i) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i) * scale;
+      qf[4 * i] = v.x;
+      qf[4 * i + 1] = v.y;
+      qf[4 * i + 2] = v.z;
+      qf[4 * i + 3] = v.w;
     }
-    if (tid < kAttK) ms[tid] = (k0 + tid < L) ? mask[row0 + k0 + tid] : 0;
-    __syncthreads();
+  }
+  float m_run = -INFINITY, l_run = 0.f;
+  floatx16 o0, o1;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) o0[e] = o1[e] = 0.f;
 
-    // scores for keys part*16 .. part*16+15
-    float s[16];
+  for (int k0 = 0; k0 < L; k0 += 32) {
+    const int kr = min(k0 + r, L - 1);
+    const bool kvalid = (k0 + r < L) && mask[row0 + kr] != 0;
+    const unsigned long long kbits = __ballot(kvalid);  // bit j = key k0 + j usable
+    float kf[32];
+    {
+      const float* src = qkv + (row0 + kr) * ld + H + h * kDh + hh * 32;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i);
+        kf[4 * i] = v.x;
+        kf[4 * i + 1] = v.y;
+        kf[4 * i + 2] = v.z;
+        kf[4 * i + 3] = v.w;
+      }
+    }
+    floatx16 st;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st[e] = 0.f;
+#pragma unroll
+    for (int sidx = 0; sidx < 32; ++sidx) st = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[sidx], qf[sidx], st, 0, 0, 0);
+
     float tmax = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int kj = part * 16 + j;
-      float acc = 0.f;
-#pragma unroll 16
-      for (int d = 0; d < kDh; ++d) acc = fmaf(qs[qi][d], ks[kj][d], acc);
-      s[j] = ms[kj] ? acc : -INFINITY;
-      tmax = fmaxf(tmax, s[j]);
+    for (int e = 0; e < 16; ++e) {
+      const int key = (e & 3) + 8 * (e >> 2) + 4 * hh;
+      st[e] = ((kbits >> key) & 1ull) ? st[e] : -INFINITY;
+      tmax = fmaxf(tmax, st[e]);
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 1));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 2));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     const float m_new = fmaxf(m_run, tmax);
-    // fully masked so far: keep everything at zero
     const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float p = (s[j] == -INFINITY) ? 0.f : expf(s[j] - m_new);
-      psum += p;
-      ps[qi][part * 16 + j] = p;
+    for (int e = 0; e < 16; ++e) {
+      st[e] = (st[e] == -INFINITY) ? 0.f : expf(st[e] - m_new);
+      psum += st[e];
     }
-    psum += __shfl_xor(psum, 1);
-    psum += __shfl_xor(psum, 2);
+    psum += __shfl_xor(psum, 32);
     l_run = l_run * alpha + psum;
     m_run = m_new;
-    __syncthreads();
+    o0 *= alpha;
+    o1 *= alpha;
+    const float* vbase = qkv + row0 * ld + 2 * H + h * kDh + r;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) o[d] *= alpha;
-    for (int j = 0; j < kAttK; ++j) {
-      const float p = ps[qi][j];
-      const float* vr = &vs[j][part * 16];
-#pragma unroll
-      for (int d = 0; d < 16; ++d) o[d] = fmaf(p, vr[d], o[d]);
+    for (int sidx = 0; sidx < 16; ++sidx) {
+      const int key = min(k0 + (sidx & 3) + 8 * (sidx >> 2) + 4 * hh, L - 1);
+      const float v0 = vbase[(int64_t)key * ld];
+      const float v1 = vbase[(int64_t)key * ld + 32];
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, st[sidx], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, st[sidx], o1, 0, 0, 0);
     }
   }
-  if (q0 + qi < L) {
-    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
-    float* dst = ctx + (row0 + q0 + qi) * H + h * kDh + part * 16;
+  // O^T (d on registers, query on lanes) -> LDS [query][d] -> coalesced row stores
+  const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
 #pragma unroll
-    for (int d = 0; d < 16; d += 4) {
-      floatx4 v = {o[d] * inv, o[d + 1] * inv, o[d + 2] * inv, o[d + 3] * inv};
-      *reinterpret_cast<floatx4*>(dst + d) = v;
-    }
+  for (int e = 0; e < 16; ++e) {
+    const int d = (e & 3) + 8 * (e >> 2) + 4 * hh;
+    obuf[r][d] = o0[e] * inv;
+    obuf[r][d + 32] = o1[e] * inv;
   }
+  __syncthreads();
+  const int nrows = min(32, L - q0);
+  for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
 }
 
 // --------------------------------------------------------------- K7 pool -----
@@ -341,6 +343,70 @@ int64_t weight_count(const mq_bert_config& c) {
 
 }  // namespace
 
+
+namespace {
+
+struct GemmArgs {
+  const float* A;
+  int lda;
+  const float* W;
+  const float* bias;
+  const float* resid;
+  int ldr;
+  float* out;
+  int ldo;
+  int M, N, K;
+};
+
+template <class T, int EPI>
+void launch_gemm_t(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(tiles), dim3(256), 0, s, g.A, g.lda, g.W,
+                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
+}
+
+using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128
+using GemmT96 = F32Tile<4, 1, 1, 3>;    // 128 x 96
+using GemmMid = F32Tile<2, 2, 2, 1>;    // 128 x 64
+using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few rows)
+
+// Pick the tile whose launch wastes the least: every CU runs two workgroups at a time,
+// so a grid that is not a multiple of 2*CUs idles part of the chip in its last round
+// (M = 8192: N = 768 -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost model:
+// rounds * tile area / relative tile efficiency.
+template <int EPI>
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s) {
+  struct Cand {
+    int bm, bn;
+    double eff;
+  };
+  const Cand cands[4] = {{128, 128, 1.0}, {128, 96, 0.96}, {128, 64, 0.9}, {32, 128, 0.55}};
+  const int64_t slots = 2 * (int64_t)num_cus;
+  int best = 0;
+  double best_cost = 1e300;
+  for (int i = 0; i < 4; ++i) {
+    const int64_t tiles = (int64_t)((g.M + cands[i].bm - 1) / cands[i].bm) * ((g.N + cands[i].bn - 1) / cands[i].bn);
+    const int64_t rounds = (tiles + slots - 1) / slots;
+    const double cost = (double)rounds * cands[i].bm * cands[i].bn / cands[i].eff;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = i;
+    }
+  }
+  switch (best) {
+    case 0: launch_gemm_t<GemmBig, EPI>(g, s); break;
+    case 1: launch_gemm_t<GemmT96, EPI>(g, s); break;
+    case 2: launch_gemm_t<GemmMid, EPI>(g, s); break;
+    default: launch_gemm_t<GemmSmall, EPI>(g, s); break;
+  }
+}
+
+// Stage labels for the optional per-kernel-class event timeline.
+enum Stage { ST_EMBED = 0, ST_QKV, ST_ATTN, ST_OPROJ, ST_LN, ST_FFN_UP, ST_FFN_DOWN, ST_POOL, ST_N };
+
+
+}  // namespace
+
 struct mq_encoder {
   int device = 0;
   mq_bert_config cfg{};
@@ -353,63 +419,68 @@ struct mq_encoder {
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
+  Timeline tl;
+  int num_cus = 256;
   std::mutex mu;
 };
 
 namespace {
 
-template <class T, int EPI>
-void launch_gemm_t(const float* A, const float* W, const float* bias, const float* resid, float* out,
-                   int M, int N, int K, hipStream_t s) {
-  const int tiles = ((M + T::BM - 1) / T::BM) * ((N + T::BN - 1) / T::BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(tiles), dim3(256), 0, s, A, W, bias, resid,
-                     out, M, N, K);
-}
-
-using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128
-using GemmMid = F32Tile<2, 2, 2, 1>;    // 128 x 64  (N = hidden: 3x the blocks)
-using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few tokens)
-
 template <int EPI>
-void launch_gemm(const float* A, const float* W, const float* bias, const float* resid, float* out,
-                 int M, int N, int K, int num_cus, hipStream_t s) {
-  const int64_t big_tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  if (M <= 64)
-    launch_gemm_t<GemmSmall, EPI>(A, W, bias, resid, out, M, N, K, s);
-  else if (big_tiles < 2 * num_cus)
-    launch_gemm_t<GemmMid, EPI>(A, W, bias, resid, out, M, N, K, s);
-  else
-    launch_gemm_t<GemmBig, EPI>(A, W, bias, resid, out, M, N, K, s);
+void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
+  e->tl.mark(s, stage);
+  launch_gemm<EPI>(g, e->num_cus, s);
 }
 
+// One forward.  With CLS pooling the last layer only needs the CLS rows after its
+// attention: its QKV projection runs on all tokens (keys / values), attention on the
+// first 32-query tile, and the output projection, LayerNorms and FFN on the B CLS
+// rows (strided views of the activations) - identical CLS outputs, ~8% less work.
 template <int VPL>
 int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, float* out,
                 hipStream_t s) {
   const mq_bert_config& c = e->cfg;
   const int M = B * L, H = c.hidden, F = c.ffn;
-  int cus = 256;
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device);
   const unsigned row_blocks = (unsigned)((M + 3) / 4);
+  const float scale = 1.0f / sqrtf((float)(H / c.heads));
+  const int q_tiles = (L + 31) / 32;
+  e->tl.mark(s, ST_EMBED);
   hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, ids, M, L,
                      c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p);
-  const float scale = 1.0f / sqrtf((float)(H / c.heads));
-  for (const LayerW& w : e->layers) {
-    launch_gemm<EPI_BIAS>(e->x.p, w.wqkv, w.bqkv, nullptr, e->qkv.p, M, 3 * H, H, cus, s);
-    hipLaunchKernelGGL(attention_kernel, dim3((L + kAttQ - 1) / kAttQ, c.heads, B), dim3(256), 0,
-                       s, e->qkv.p, mask, L, H, scale, e->ctx.p);
-    launch_gemm<EPI_RESID>(e->ctx.p, w.wo, w.bo, e->x.p, e->y.p, M, H, H, cus, s);
-    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, e->y.p, M, w.ln1g,
-                       w.ln1b, c.ln_eps, e->x.p);
+  for (size_t li = 0; li < e->layers.size(); ++li) {
+    const LayerW& w = e->layers[li];
+    const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
+    // rows this layer carries past attention: all M tokens, or the B CLS rows
+    const int rows = cls_only ? B : M;
+    const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
+    const unsigned rb = (unsigned)((rows + 3) / 4);
+    gemm<EPI_BIAS>(e, {e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+                   ST_QKV, s);
+    e->tl.mark(s, ST_ATTN);
+    const int qt = cls_only ? 1 : q_tiles;
+    hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
+                       H, c.heads, qt, scale, e->ctx.p);
+    // y = x + ctx Wo^T + bo  (compact [rows, H])
+    gemm<EPI_RESID>(e, {e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
+                    ST_OPROJ, s);
+    e->tl.mark(s, ST_LN);
+    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln1g, w.ln1b,
+                       c.ln_eps, e->x.p);
+    const GemmArgs up{e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
     if (c.gelu == MQ_GELU_TANH)
-      launch_gemm<EPI_GELU_TANH>(e->x.p, w.w1, w.b1, nullptr, e->ffn.p, M, F, H, cus, s);
+      gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s);
     else
-      launch_gemm<EPI_GELU_ERF>(e->x.p, w.w1, w.b1, nullptr, e->ffn.p, M, F, H, cus, s);
-    launch_gemm<EPI_RESID>(e->ffn.p, w.w2, w.b2, e->x.p, e->y.p, M, H, F, cus, s);
-    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, e->y.p, M, w.ln2g,
-                       w.ln2b, c.ln_eps, e->x.p);
+      gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
+    gemm<EPI_RESID>(e, {e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F}, ST_FFN_DOWN, s);
+    e->tl.mark(s, ST_LN);
+    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln2g, w.ln2b,
+                       c.ln_eps, e->x.p);
   }
-  hipLaunchKernelGGL((pool_kernel<VPL>), dim3((B + 3) / 4), dim3(256), 0, s, e->x.p, mask, B, L,
-                     c.pooling, out);
+  e->tl.mark(s, ST_POOL);
+  const bool pruned = c.pooling == MQ_POOL_CLS;  // x holds [B, H] CLS rows
+  hipLaunchKernelGGL((pool_kernel<VPL>), dim3((B + 3) / 4), dim3(256), 0, s, e->x.p, mask, B,
+                     pruned ? 1 : L, c.pooling, out);
+  e->tl.close(s);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -442,6 +513,10 @@ int mq_encoder_create(int device, const mq_bert_config* cfg, mq_encoder** out) {
   auto e = std::make_unique<mq_encoder>();
   e->device = device;
   e->cfg = c;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      cus > 0)
+    e->num_cus = cus;
   *out = e.release();
   return MQ_OK;
 }
@@ -512,6 +587,25 @@ int mq_encoder_set_precision(mq_encoder* e, int dtype) {
   return MQ_OK;
 }
 
+int mq_encoder_set_timing(mq_encoder* e, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(e, "NULL encoder");
+  std::lock_guard<std::mutex> lk(e->mu);
+  DeviceGuard dg(e->device);
+  e->tl.drain();
+  e->tl.on = enabled != 0;
+  return MQ_OK;
+}
+
+int mq_encoder_read_timing(mq_encoder* e, float* ms, int n) {
+  clear_error();
+  MQ_CHECK_ARG(e && ms && n >= 0, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  DeviceGuard dg(e->device);
+  e->tl.read(ms, n);
+  return MQ_OK;
+}
+
 int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int B, int L,
                      float* out, int io_on_device, void* stream) {
   clear_error();
@@ -527,6 +621,7 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   hipStream_t s = (hipStream_t)stream;
   const mq_bert_config& c = e->cfg;
   const size_t M = (size_t)B * L;
+  if (e->tl.used > 4096) e->tl.drain();  // bound the event pool while timing
   int rc = MQ_OK;
   for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, M * c.hidden),
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),

@@ -39,37 +39,47 @@ struct F32Tile {
 };
 
 // One K-slice of both operands, held in registers between the global load and the
-// LDS write (T14 "issue early / write late").
+// LDS write (T14 "issue early / write late").  Row pointers are resolved once per
+// tile (`bind`): out-of-range rows are clamped to a valid row and zeroed after the
+// load, so the per-slice path is branch-free: 8 x global_load_dwordx4 + selects.
 template <class T>
 struct Stager {
   floatx4 r[T::LOADS];
+  const float* src[T::LOADS];
+  bool ok[T::LOADS];
 
-  // A rows m0.. (valid < M), B rows n0.. (valid < N), columns k0 .. k0+31.
-  __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda, int M, int m0,
+  // A rows m0.. (valid < M), B rows n0.. (valid < N).
+  __device__ __forceinline__ void bind(const float* __restrict__ A, int64_t lda, int M, int m0,
                                        const float* __restrict__ B, int64_t ldb, int64_t N,
-                                       int64_t n0, int k0, int tid) {
+                                       int64_t n0, int tid) {
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
       const int row = f >> 3, ch = f & 7;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (i < T::BM / 32) {  // compile-time after unrolling: rows [32i, 32i+32) are A rows
         const int gm = m0 + row;
-        if (gm < M) v = *reinterpret_cast<const floatx4*>(A + gm * lda + k0 + ch * 4);
+        ok[i] = gm < M;
+        src[i] = A + (int64_t)(ok[i] ? gm : 0) * lda + ch * 4;
       } else {
         const int64_t gn = n0 + (row - T::BM);
-        if (gn < N) v = *reinterpret_cast<const floatx4*>(B + gn * ldb + k0 + ch * 4);
+        ok[i] = gn < N;
+        src[i] = B + (ok[i] ? gn : 0) * ldb + ch * 4;
       }
-      r[i] = v;
     }
   }
 
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int i = 0; i < T::LOADS; ++i) r[i] = *reinterpret_cast<const floatx4*>(src[i] + k0);
+  }
+
   __device__ __forceinline__ void store(float* stage, int tid) const {
+    const floatx4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
       const int row = f >> 3, ch = f & 7;
-      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = r[i];
+      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = ok[i] ? r[i] : z;
     }
   }
 };

@@ -84,34 +84,36 @@ struct TopList {
 
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
-using SearchNarrow = F32Tile<1, 4, 1, 2>;  // 32 queries x 256 rows per block (small batches)
+using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
 
 template <class T>
 struct SearchSmem {
-  static constexpr int SCORE_STRIDE = T::WN + 4;  // 68 floats: conflict-free row scans
-  static constexpr int SCORE_FLOATS = T::WM * SCORE_STRIDE;  // per wave
-  static constexpr int FLOATS = 2 * T::STAGE_FLOATS + 4 * SCORE_FLOATS;
-  static constexpr int LPQ = kWave / T::WM;  // lanes scanning one query row
-  static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget");
+  // The finished wave tile is scanned in TN passes of 32 columns; each pass parks the
+  // wave's [WM][32] scores in the LDS stage buffer the last K-slice just released
+  // (row stride 36 floats = 144 B: conflict-free ds_read_b128 row scans).
+  static constexpr int SCORE_STRIDE = 36;
+  static constexpr int SCORE_FLOATS = T::WM * SCORE_STRIDE;  // per wave per pass
+  static constexpr int LPQ = kWave / T::WM;                   // lanes scanning one query row
+  static constexpr int COLS = 32 / LPQ;                       // columns per lane per pass
+  static_assert(4 * SCORE_FLOATS <= T::STAGE_FLOATS, "score tile must fit a stage buffer");
+  static_assert(2 * T::STAGE_FLOATS * 4 <= 80 * 1024, "two workgroups per CU");
 };
 
 // Grid: nqt query tiles x G row groups (G % 8 == 0).  Block (qt, g) scans row tiles
 // g, g+G, g+2G, ... for queries [qt*BM, qt*BM + BM) and leaves, per lane, the top-k of
 // what it saw in cand[list][query][0..k) with list = (g*WAVES_N + wn)*LPQ + part.
-// Scores never leave the chip: each finished BMxBN tile goes accumulator -> per-wave
-// LDS tile -> one lane per (query, part) scans its row against its register top-k.
+// Scores never leave the chip: each finished tile goes accumulator -> LDS (the stage
+// buffer the last slice released) -> one lane per (query, part) scans its row against
+// its register top-KC list; only beating the list tail costs an insertion.
 template <class T, int KC>
-__global__ __launch_bounds__(256, 1) void flat_search_kernel(
+__global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
     const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
     int G, int nqt, int k, float* __restrict__ cand_s, int* __restrict__ cand_i) {
   using S = SearchSmem<T>;
-  __shared__ __attribute__((aligned(16))) float lds[S::FLOATS];
-  float* stage0 = lds;
-  float* stage1 = lds + T::STAGE_FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
-  float* score = lds + 2 * T::STAGE_FLOATS + wave * S::SCORE_FLOATS;
 
   // blocks b and b+8 share an XCD: give the nqt query tiles of one row group to one
   // XCD so the second read of each row tile is an L2 hit.
@@ -120,9 +122,7 @@ __global__ __launch_bounds__(256, 1) void flat_search_kernel(
   const int m0 = qt * T::BM;
   const int64_t ntiles = (n_rows + T::BN - 1) / T::BN;
   const int nk = dim / kBK;
-
   const int q_local = lane % T::WM, part = lane / T::WM;
-  constexpr int COLS = T::WN / S::LPQ;  // columns of the wave tile this lane scans
 
   TopList<KC> top;
   top.init();
@@ -130,8 +130,9 @@ __global__ __launch_bounds__(256, 1) void flat_search_kernel(
   int64_t t = g;
   if (t < ntiles) {
     Stager<T> st;
-    st.load(Q, dim, nq, m0, C, dim, n_rows, t * T::BN, 0, tid);
-    st.store(stage0, tid);
+    st.bind(Q, dim, nq, m0, C, dim, n_rows, t * T::BN, tid);
+    st.load(0);
+    st.store(lds, tid);
     __syncthreads();
     int buf = 0;
     floatx16 acc[T::TM][T::TN];
@@ -140,36 +141,37 @@ __global__ __launch_bounds__(256, 1) void flat_search_kernel(
       for (int kt = 0; kt < nk; ++kt) {
         // prefetch the next slice: (t, kt+1) or the first slice of the next row tile
         const bool same = kt + 1 < nk;
-        const int64_t tn = same ? t : t + G;
-        const bool more = same || tn < ntiles;
-        if (more) st.load(Q, dim, nq, m0, C, dim, n_rows, tn * T::BN, same ? (kt + 1) * kBK : 0, tid);
-        mma_slice<T>(buf ? stage1 : stage0, acc, wm, wn, lane);
-        if (more) st.store(buf ? stage0 : stage1, tid);
+        const bool more = same || t + G < ntiles;
+        if (!same && more) st.bind(Q, dim, nq, m0, C, dim, n_rows, (t + G) * T::BN, tid);
+        if (more) st.load(same ? (kt + 1) * kBK : 0);
+        mma_slice<T>(lds + buf * T::STAGE_FLOATS, acc, wm, wn, lane);
+        if (more) st.store(lds + (buf ^ 1) * T::STAGE_FLOATS, tid);
         __syncthreads();
         buf ^= 1;
       }
-      // ---- epilogue: wave tile -> LDS [query][row] (rows beyond n_rows = -inf)
+      // ---- epilogue in the released stage buffer: per wave [WM][32] per pass
+      float* score = lds + (buf ^ 1) * T::STAGE_FLOATS + wave * S::SCORE_FLOATS;
       const int64_t col0 = t * T::BN + wn * T::WN;
 #pragma unroll
-      for (int tm = 0; tm < T::TM; ++tm)
+      for (int tn2 = 0; tn2 < T::TN; ++tn2) {
 #pragma unroll
-        for (int tn2 = 0; tn2 < T::TN; ++tn2) {
-          const int c = tn2 * 32 + (lane & 31);
-          const bool valid = col0 + c < n_rows;
+        for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
           for (int e = 0; e < 16; ++e)
-            score[acc_row(tm, e, lane) * S::SCORE_STRIDE + c] = valid ? acc[tm][tn2][e] : -INFINITY;
-        }
-      __syncthreads();
-      const float* row = score + q_local * S::SCORE_STRIDE + part * COLS;
+            score[acc_row(tm, e, lane) * S::SCORE_STRIDE + (lane & 31)] = acc[tm][tn2][e];
+        __syncthreads();
+        const float* row = score + q_local * S::SCORE_STRIDE + part * S::COLS;
+        const int64_t c0 = col0 + tn2 * 32 + part * S::COLS;
 #pragma unroll
-      for (int c4 = 0; c4 < COLS; c4 += 4) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
+        for (int c4 = 0; c4 < S::COLS; c4 += 4) {
+          const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t col = col0 + part * COLS + c4 + e;
-          if (col < n_rows && top.beats_tail(v[e], (int)col)) top.insert(v[e], (int)col);
+          for (int e = 0; e < 4; ++e) {
+            const int64_t col = c0 + c4 + e;
+            if (col < n_rows && top.beats_tail(v[e], (int)col)) top.insert(v[e], (int)col);
+          }
         }
+        __syncthreads();
       }
       t += G;
       if (t >= ntiles) break;
@@ -324,6 +326,7 @@ struct mq_index {
   float* rows = nullptr;  // [cap, dim], every stored row unit-norm
   int num_cus = 256;
   DevBuf stage, cand_s, cand_i, out_s, out_i;
+  Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   std::mutex mu;
 };
 
@@ -360,7 +363,7 @@ struct SearchPlan {
   int64_t n_lists;
 };
 
-SearchPlan plan_search(const mq_index* ix, int64_t nq) {
+SearchPlan plan_search(const mq_index* ix, int64_t nq, int k) {
   SearchPlan p;
   p.wide = nq > 64;
   const int BM = p.wide ? SearchWide::BM : SearchNarrow::BM;
@@ -369,8 +372,10 @@ SearchPlan plan_search(const mq_index* ix, int64_t nq) {
   const int lpq = p.wide ? SearchSmem<SearchWide>::LPQ : SearchSmem<SearchNarrow>::LPQ;
   p.nqt = (int)((nq + BM - 1) / BM);
   const int64_t ntiles = (ix->n + BN - 1) / BN;
-  // one 256-thread block per CU: G row groups per query tile, a multiple of 8
-  int64_t G = std::max<int64_t>(1, ix->num_cus / p.nqt);
+  // resident 256-thread blocks per CU: 2 with the 8-entry register top list, else 1
+  // (VGPR budget); G row groups per query tile, a multiple of 8 (XCD mapping)
+  const int per_cu = kc_for(k) <= 8 ? 2 : 1;
+  int64_t G = std::max<int64_t>(1, per_cu * ix->num_cus / p.nqt);
   G = std::min<int64_t>(G, ntiles);
   p.G = (int)((G + 7) / 8 * 8);
   p.n_lists = (int64_t)p.G * wn * lpq;
@@ -390,7 +395,7 @@ int fill_padding(float* os, int64_t* oi, int64_t count, hipStream_t s) {
 int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                   hipStream_t s) {
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
-  const SearchPlan p = plan_search(ix, nq);
+  const SearchPlan p = plan_search(ix, nq, k);
   const size_t n_cand = (size_t)p.n_lists * nq * k;
   int rc = ix->cand_s.ensure(n_cand * sizeof(float));
   if (rc) return rc;
@@ -405,6 +410,8 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
     case 32: launch_search<T, 32>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
     default: launch_search<T, 64>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
   }
+  if (ix->tl.used > 4096) ix->tl.drain();
+  ix->tl.mark(s, 0);
   if (p.wide) {
     MQ_SEARCH(SearchWide)
   } else {
@@ -412,7 +419,9 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
   }
 #undef MQ_SEARCH
   MQ_HIP(hipGetLastError());
+  ix->tl.mark(s, 1);
   merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, k, k, os, oi, s);
+  ix->tl.close(s);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -591,6 +600,25 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
   MQ_HIP(hipMemcpyAsync(out, ix->rows + row0 * ix->dim, (size_t)n * ix->dim * 4,
                         out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
   if (!out_on_device) MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_index_set_timing(mq_index* ix, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  ix->tl.drain();
+  ix->tl.on = enabled != 0;
+  return MQ_OK;
+}
+
+int mq_index_read_timing(mq_index* ix, float* ms, int n) {
+  clear_error();
+  MQ_CHECK_ARG(ix && ms && n >= 0, "bad argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  ix->tl.read(ms, n);
   return MQ_OK;
 }
 

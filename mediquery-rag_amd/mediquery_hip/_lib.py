@@ -60,6 +60,8 @@ SIGNATURES = {
     "mq_index_search": (_I, [_P, _P, _I64, _I, _P, _P, _I, _P]),
     "mq_index_get": (_I, [_P, _I64, _I64, _P, _I, _P]),
     "mq_index_data": (_I, [_P, _PP]),
+    "mq_index_set_timing": (_I, [_P, _I]),
+    "mq_index_read_timing": (_I, [_P, _P, _I]),
     "mq_index_save": (_I, [_P, ctypes.c_char_p]),
     "mq_index_load": (_I, [_P, ctypes.c_char_p]),
     "mq_topk_merge_host": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P]),
@@ -69,6 +71,8 @@ SIGNATURES = {
     "mq_encoder_weight_count": (_I64, [ctypes.POINTER(BertConfigC)]),
     "mq_encoder_load_weights": (_I, [_P, _P, _I64]),
     "mq_encoder_set_precision": (_I, [_P, _I]),
+    "mq_encoder_set_timing": (_I, [_P, _I]),
+    "mq_encoder_read_timing": (_I, [_P, _P, _I]),
     "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),
 }
 

@@ -72,6 +72,17 @@ class FlatIndex:
         _lib.call("mq_index_data", self._h, ctypes.byref(p))
         return p.value
 
+    STAGES = ("flat_search_kernel", "merge_kernel")
+
+    def set_timing(self, enabled=True):
+        _lib.call("mq_index_set_timing", self._h, int(bool(enabled)))
+
+    def read_timing(self):
+        """{stage: device ms since the last read} (HIP events on the launch stream)."""
+        ms = np.zeros(len(self.STAGES), dtype=np.float32)
+        _lib.call("mq_index_read_timing", self._h, _lib.ptr(ms), len(ms))
+        return dict(zip(self.STAGES, ms.tolist()))
+
     def save(self, path):
         _lib.call("mq_index_save", self._h, str(path).encode())
 
@@ -124,6 +135,17 @@ class Encoder:
                 pass
 
     __del__ = close
+
+    STAGES = ("embed_ln", "qkv_gemm", "attention", "out_proj_gemm", "layernorm", "ffn_up_gemm",
+              "ffn_down_gemm", "pool")
+
+    def set_timing(self, enabled=True):
+        _lib.call("mq_encoder_set_timing", self._h, int(bool(enabled)))
+
+    def read_timing(self):
+        ms = np.zeros(len(self.STAGES), dtype=np.float32)
+        _lib.call("mq_encoder_read_timing", self._h, _lib.ptr(ms), len(ms))
+        return dict(zip(self.STAGES, ms.tolist()))
 
     def set_precision(self, dtype):
         _lib.call("mq_encoder_set_precision", self._h, dtype)
