@@ -41,6 +41,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 // out[M,N] = epi(A[M,K] . W[N,K]^T + bias[N] (+ resid[M,N])), K % 32 == 0.
 // Row strides lda / ldr / ldo (in floats) let the CLS-only last layer run on every
 // L-th row of the activations without a gather.
+// Persistent: gridDim.x workgroups (a multiple of 8, two per CU) walk the tiles
+// t = blockIdx.x, +gridDim.x, ...; the first K-slice of the next tile is fetched during
+// the last slice of the current one, so the epilogue overlaps the next tile's loads.
+// Within a round, the workgroups of one XCD (blockIdx % 8 equal) take consecutive
+// tiles, i.e. share A row panels in their L2.
 template <class T, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
@@ -49,47 +54,62 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
                                                          float* __restrict__ out, int ldo, int M,
                                                          int N, int K) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
-  float* stage0 = lds;
-  float* stage1 = lds + T::STAGE_FLOATS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
   const int tiles_n = (N + T::BN - 1) / T::BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);  // neighbours share the A panel on one XCD
-  const int m0 = (wg / tiles_n) * T::BM, n0 = (wg % tiles_n) * T::BN;
+  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
+  const int G = gridDim.x, per_xcd = G >> 3;
+  const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   const int nk = K / kBK;
+  auto tile_of = [&](int round) { return round * G + xslot; };
 
-  floatx16 acc[T::TM][T::TN];
-  zero_acc<T>(acc);
+  int round = 0;
+  int t = tile_of(0);
+  if (t >= total) return;
   Stager<T> st;
-  st.bind(A, lda, M, m0, W, K, N, n0, tid);
+  st.bind(A, lda, M, (t / tiles_n) * T::BM, W, K, N, (t % tiles_n) * T::BN, tid);
   st.load(0);
-  st.store(stage0, tid);
+  st.store(lds, tid);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) st.load((kt + 1) * kBK);
-    mma_slice<T>((kt & 1) ? stage1 : stage0, acc, wm, wn, lane);
-    if (more) st.store((kt & 1) ? stage0 : stage1, tid);
-    __syncthreads();
-  }
-
+  int buf = 0;
+  while (true) {
+    const int m0 = (t / tiles_n) * T::BM, n0 = (t % tiles_n) * T::BN;
+    const int t_next = tile_of(round + 1);
+    floatx16 acc[T::TM][T::TN];
+    zero_acc<T>(acc);
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool same = kt + 1 < nk;
+      const bool more = same || t_next < total;
+      if (!same && more)
+        st.bind(A, lda, M, (t_next / tiles_n) * T::BM, W, K, N, (t_next % tiles_n) * T::BN, tid);
+      if (more) st.load(same ? (kt + 1) * kBK : 0);
+      mma_slice<T>(lds + buf * T::STAGE_FLOATS, acc, wm, wn, lane);
+      if (more) st.store(lds + (buf ^ 1) * T::STAGE_FLOATS, tid);
+      __syncthreads();
+      buf ^= 1;
+    }
 #pragma unroll
-  for (int tn = 0; tn < T::TN; ++tn) {
-    const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
-    if (col >= N) continue;
-    const float b = bias[col];
+    for (int tn = 0; tn < T::TN; ++tn) {
+      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
+      if (col < N) {
+        const float b = bias[col];
 #pragma unroll
-    for (int tm = 0; tm < T::TM; ++tm)
+        for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
-        if (row >= M) continue;
-        float v = acc[tm][tn][e] + b;
-        if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-        if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-        if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
-        out[(int64_t)row * ldo + col] = v;
+          for (int e = 0; e < 16; ++e) {
+            const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
+            if (row >= M) continue;
+            float v = acc[tm][tn][e] + b;
+            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+            if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+            out[(int64_t)row * ldo + col] = v;
+          }
       }
+    }
+    ++round;
+    t = t_next;
+    if (t >= total) break;
   }
 }
 
@@ -359,9 +379,11 @@ struct GemmArgs {
 };
 
 template <class T, int EPI>
-void launch_gemm_t(const GemmArgs& g, hipStream_t s) {
+void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s) {
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(tiles), dim3(256), 0, s, g.A, g.lda, g.W,
+  // persistent grid: at most two workgroups per CU, rounded up to a multiple of 8
+  const int grid = (std::min(tiles, 2 * num_cus) + 7) / 8 * 8;
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
                      g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
 }
 
@@ -374,6 +396,16 @@ using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few rows)
 // so a grid that is not a multiple of 2*CUs idles part of the chip in its last round
 // (M = 8192: N = 768 -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost model:
 // rounds * tile area / relative tile efficiency.
+template <int EPI>
+void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
+  switch (tile) {
+    case 0: launch_gemm_t<GemmBig, EPI>(g, num_cus, s); break;
+    case 1: launch_gemm_t<GemmT96, EPI>(g, num_cus, s); break;
+    case 2: launch_gemm_t<GemmMid, EPI>(g, num_cus, s); break;
+    default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); break;
+  }
+}
+
 template <int EPI>
 void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s) {
   struct Cand {
@@ -393,12 +425,7 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s) {
       best = i;
     }
   }
-  switch (best) {
-    case 0: launch_gemm_t<GemmBig, EPI>(g, s); break;
-    case 1: launch_gemm_t<GemmT96, EPI>(g, s); break;
-    case 2: launch_gemm_t<GemmMid, EPI>(g, s); break;
-    default: launch_gemm_t<GemmSmall, EPI>(g, s); break;
-  }
+  launch_gemm_tile<EPI>(g, best, num_cus, s);
 }
 
 // Stage labels for the optional per-kernel-class event timeline.
@@ -584,6 +611,27 @@ int mq_encoder_set_precision(mq_encoder* e, int dtype) {
   MQ_CHECK_ARG(e, "NULL encoder");
   MQ_CHECK_ARG(dtype == MQ_DTYPE_F32, "only the f32 encoder path is implemented (got %d)", dtype);
   e->precision = dtype;
+  return MQ_OK;
+}
+
+int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
+                      float* out, int M, int N, int K, int epi, int tile, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
+  MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 3, "bad epi/tile");
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const GemmArgs g{A, K, W, bias, resid, N, out, N, M, N, K};
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case EPI_BIAS: launch_gemm_tile<EPI_BIAS>(g, tile, cus, s); break;
+    case EPI_GELU_ERF: launch_gemm_tile<EPI_GELU_ERF>(g, tile, cus, s); break;
+    case EPI_GELU_TANH: launch_gemm_tile<EPI_GELU_TANH>(g, tile, cus, s); break;
+    default: launch_gemm_tile<EPI_RESID>(g, tile, cus, s); break;
+  }
+  MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
 

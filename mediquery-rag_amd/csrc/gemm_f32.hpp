@@ -40,15 +40,15 @@ struct F32Tile {
 
 // One K-slice of both operands, held in registers between the global load and the
 // LDS write (T14 "issue early / write late").  Row pointers are resolved once per
-// tile (`bind`): out-of-range rows are clamped to a valid row and zeroed after the
-// load, so the per-slice path is branch-free: 8 x global_load_dwordx4 + selects.
+// tile (`bind`).  Rows past M / N are clamped onto the last valid row instead of being
+// zeroed: an MFMA output element depends only on its own A row and B row, so the
+// garbage lands only in output rows / columns the epilogue never stores.  The per-slice
+// path is therefore LOADS x global_load_dwordx4 and nothing else.
 template <class T>
 struct Stager {
   floatx4 r[T::LOADS];
   const float* src[T::LOADS];
-  bool ok[T::LOADS];
 
-  // A rows m0.. (valid < M), B rows n0.. (valid < N).
   __device__ __forceinline__ void bind(const float* __restrict__ A, int64_t lda, int M, int m0,
                                        const float* __restrict__ B, int64_t ldb, int64_t N,
                                        int64_t n0, int tid) {
@@ -57,13 +57,11 @@ struct Stager {
       const int f = tid + i * T::THREADS;
       const int row = f >> 3, ch = f & 7;
       if (i < T::BM / 32) {  // compile-time after unrolling: rows [32i, 32i+32) are A rows
-        const int gm = m0 + row;
-        ok[i] = gm < M;
-        src[i] = A + (int64_t)(ok[i] ? gm : 0) * lda + ch * 4;
+        const int gm = min(m0 + row, M - 1);
+        src[i] = A + (int64_t)gm * lda + ch * 4;
       } else {
-        const int64_t gn = n0 + (row - T::BM);
-        ok[i] = gn < N;
-        src[i] = B + (ok[i] ? gn : 0) * ldb + ch * 4;
+        const int64_t gn = min(n0 + (row - T::BM), N - 1);
+        src[i] = B + gn * ldb + ch * 4;
       }
     }
   }
@@ -74,12 +72,11 @@ struct Stager {
   }
 
   __device__ __forceinline__ void store(float* stage, int tid) const {
-    const floatx4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
       const int row = f >> 3, ch = f & 7;
-      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = ok[i] ? r[i] : z;
+      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = r[i];
     }
   }
 };

@@ -74,6 +74,7 @@ SIGNATURES = {
     "mq_encoder_set_timing": (_I, [_P, _I]),
     "mq_encoder_read_timing": (_I, [_P, _P, _I]),
     "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),
+    "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }
 
 _lib = None

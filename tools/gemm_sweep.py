@@ -1,0 +1,46 @@
+"""Time the fp32 MFMA GEMM core per tile geometry on the encoder's shapes (B=256, L=32)
+through the mq_debug_gemm_f32 hook.  Prints TFLOP/s per (shape, tile)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mediquery-rag_amd"), ROOT]
+import torch  # noqa: E402
+from mediquery_hip import _lib  # noqa: E402
+
+SHAPES = {"qkv": (8192, 2304, 768), "out_proj": (8192, 768, 768), "ffn_up": (8192, 3072, 768),
+          "ffn_down": (8192, 768, 3072)}
+TILES = ["128x128", "128x96", "128x64", "32x128"]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    res = {}
+    for name, (M, N, K) in SHAPES.items():
+        A = torch.randn(M, K, device=dev)
+        W = torch.randn(N, K, device=dev) * 0.05
+        b = torch.randn(N, device=dev)
+        R = torch.randn(M, N, device=dev)
+        out = torch.empty(M, N, device=dev)
+        epi = 1 if name == "ffn_up" else (3 if name in ("out_proj", "ffn_down") else 0)
+        for t, tname in enumerate(TILES):
+            def run():
+                _lib.call("mq_debug_gemm_f32", _lib.ptr(A), _lib.ptr(W), _lib.ptr(b), _lib.ptr(R),
+                          _lib.ptr(out), M, N, K, epi, t, _lib.stream_handle())
+            for _ in range(3):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 20
+            e0.record()
+            for _ in range(n):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / n
+            res["%s/%s" % (name, tname)] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
