@@ -140,7 +140,8 @@ int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, i
 /* ------------------------------------------------------- testing hooks ---- */
 /* One encoder GEMM on device buffers: out[M,N] = epi(A[M,K] W[N,K]^T + bias (+ resid)),
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,
- * 1 = 128x96, 2 = 128x64, 3 = 32x128.  K % 32 == 0.  For kernel unit tests. */
+ * 1 = 128x96, 2 = 128x64, 3 = 32x128, 4 = split-K (32x128 tiles + ordered slab
+ * reduction; synchronous, N % 4 == 0).  K % 32 == 0.  For kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
 

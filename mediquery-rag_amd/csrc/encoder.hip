@@ -54,63 +54,107 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
                                                          float* __restrict__ out, int ldo, int M,
                                                          int N, int K) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
   const int tiles_n = (N + T::BN - 1) / T::BN;
   const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
   const int G = gridDim.x, per_xcd = G >> 3;
   const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int nk = K / kBK;
-  auto tile_of = [&](int round) { return round * G + xslot; };
-
-  int round = 0;
-  int t = tile_of(0);
-  if (t >= total) return;
-  Stager<T> st;
-  st.bind(A, lda, M, (t / tiles_n) * T::BM, W, K, N, (t % tiles_n) * T::BN, tid);
-  st.load(0);
-  st.store(lds, tid);
-  __syncthreads();
-  int buf = 0;
-  while (true) {
-    const int m0 = (t / tiles_n) * T::BM, n0 = (t % tiles_n) * T::BN;
-    const int t_next = tile_of(round + 1);
-    floatx16 acc[T::TM][T::TN];
-    zero_acc<T>(acc);
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool same = kt + 1 < nk;
-      const bool more = same || t_next < total;
-      if (!same && more)
-        st.bind(A, lda, M, (t_next / tiles_n) * T::BM, W, K, N, (t_next % tiles_n) * T::BN, tid);
-      if (more) st.load(same ? (kt + 1) * kBK : 0);
-      mma_slice<T>(lds + buf * T::STAGE_FLOATS, acc, wm, wn, lane);
-      if (more) st.store(lds + (buf ^ 1) * T::STAGE_FLOATS, tid);
-      __syncthreads();
-      buf ^= 1;
-    }
+  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
+  auto coords = [&](int i, int& m0, int64_t& n0) {
+    const int t = i * G + xslot;
+    m0 = (t / tiles_n) * T::BM;
+    n0 = (int64_t)(t % tiles_n) * T::BN;
+  };
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
+    int m0;
+    int64_t n0l;
+    coords(i, m0, n0l);
+    const int n0 = (int)n0l;
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn) {
       const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
-      if (col < N) {
-        const float b = bias[col];
+      if (col >= N) continue;
+      const float b = bias[col];
 #pragma unroll
-        for (int tm = 0; tm < T::TM; ++tm)
+      for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
-            if (row >= M) continue;
-            float v = acc[tm][tn][e] + b;
-            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-            if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
-            out[(int64_t)row * ldo + col] = v;
-          }
-      }
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
+          if (row >= M) continue;
+          float v = acc[tm][tn][e] + b;
+          if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+          if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+          if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+          out[(int64_t)row * ldo + col] = v;
+        }
     }
-    ++round;
-    t = t_next;
-    if (t >= total) break;
+  };
+  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
+}
+
+// ---------------------------------------------------------- split-K GEMM ------
+// For few rows (single queries, the CLS-only last layer) the direct GEMM leaves most
+// CUs idle.  Split K into S chunks: workgroup (tile, s) multiplies its tile over
+// K-chunk s and stores an fp32 partial slab[s][M][N]; splitk_reduce_kernel then sums
+// the S slabs IN ORDER (bitwise reproducible) and applies bias / GELU / residual.
+template <class T>
+__global__ __launch_bounds__(256, 2) void gemm_splitk_kernel(const float* __restrict__ A, int lda,
+                                                             const float* __restrict__ W, int M,
+                                                             int N, int K, int S,
+                                                             float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  const int tiles_n = (N + T::BN - 1) / T::BN;
+  const int tile = blockIdx.x / S, sidx = blockIdx.x % S;
+  const int Kc = K / S;
+  const int m0 = (tile / tiles_n) * T::BM;
+  const int n0 = (tile % tiles_n) * T::BN;
+  auto coords = [&](int, int& mm0, int64_t& nn0) {
+    mm0 = m0;
+    nn0 = n0;
+  };
+  float* dst = slab + (int64_t)sidx * M * N;
+  auto epi = [&](int, floatx16(&acc)[T::TM][T::TN], float*) {
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn) {
+      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
+      if (col >= N) continue;
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
+          if (row < M) dst[(int64_t)row * N + col] = acc[tm][tn][e];
+        }
+    }
+  };
+  walk_tiles<T>(lds, 1, TileOperands{A + (int64_t)sidx * Kc, lda, M, W + (int64_t)sidx * Kc, K, N, Kc},
+                coords, epi);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int S,
+                                                            int M, int N,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ resid, int ldr,
+                                                            float* __restrict__ out, int ldo) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index, N % 4 == 0
+  const int64_t n4 = N / 4;
+  if (i4 >= (int64_t)M * n4) return;
+  const int row = (int)(i4 / n4), c = (int)(i4 % n4) * 4;
+  const int64_t plane = (int64_t)M * N;
+  floatx4 v = *reinterpret_cast<const floatx4*>(slab + (int64_t)row * N + c);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const floatx4*>(slab + s * plane + (int64_t)row * N + c);
+  v += *reinterpret_cast<const floatx4*>(bias + c);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (EPI == EPI_GELU_ERF) v[j] = gelu_erf(v[j]);
+    if (EPI == EPI_GELU_TANH) v[j] = gelu_tanh(v[j]);
   }
+  if (EPI == EPI_RESID) v += *reinterpret_cast<const floatx4*>(resid + (int64_t)row * ldr + c);
+  *reinterpret_cast<floatx4*>(out + (int64_t)row * ldo + c) = v;
 }
 
 // ------------------------------------------------------- K1 / LayerNorm ------
@@ -367,6 +411,8 @@ int64_t weight_count(const mq_bert_config& c) {
 namespace {
 
 struct GemmArgs {
+  float* slab;  // split-K workspace (may be null: never split)
+  size_t slab_floats;
   const float* A;
   int lda;
   const float* W;
@@ -406,8 +452,38 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
   }
 }
 
+// Split-K factor for a GEMM that would under-fill the chip (0 = run it directly):
+// enough chunks for ~2 workgroups per CU, each chunk a multiple of 32 deep.
+int splitk_factor(const GemmArgs& g, int num_cus) {
+  if (!g.slab || g.N % 4 != 0) return 0;
+  const int64_t tiles = (int64_t)((g.M + 31) / 32) * ((g.N + 127) / 128);  // 32 x 128 tiles
+  const int64_t slots = 2 * (int64_t)num_cus;
+  if (tiles * 2 > slots || g.M > 256) return 0;
+  const int slices = g.K / kBK;
+  int best = 1;
+  for (int s = 1; s <= slices; ++s)
+    if (slices % s == 0 && tiles * s <= slots && (size_t)s * g.M * g.N <= g.slab_floats) best = s;
+  return best >= 2 ? best : 0;
+}
+
+template <int EPI>
+void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
+  using T = F32Tile<1, 4, 1, 1>;
+  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+  hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W,
+                     g.M, g.N, g.K, S, g.slab);
+  const int64_t n4 = (int64_t)g.M * g.N / 4;
+  hipLaunchKernelGGL((splitk_reduce_kernel<EPI>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                     s, g.slab, S, g.M, g.N, g.bias, g.resid, g.ldr, g.out, g.ldo);
+}
+
 template <int EPI>
 void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s) {
+  const int S = splitk_factor(g, num_cus);
+  if (S) {
+    launch_splitk<EPI>(g, S, s);
+    return;
+  }
   struct Cand {
     int bm, bn;
     double eff;
@@ -442,7 +518,7 @@ struct mq_encoder {
   Buf weights;
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
-  Buf x, y, qkv, ctx, ffn, io_out;
+  Buf x, y, qkv, ctx, ffn, io_out, slab;
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -481,24 +557,24 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
     const unsigned rb = (unsigned)((rows + 3) / 4);
-    gemm<EPI_BIAS>(e, {e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+    gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
                    ST_QKV, s);
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
                        H, c.heads, qt, scale, e->ctx.p);
     // y = x + ctx Wo^T + bo  (compact [rows, H])
-    gemm<EPI_RESID>(e, {e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
+    gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
                     ST_OPROJ, s);
     e->tl.mark(s, ST_LN);
     hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln1g, w.ln1b,
                        c.ln_eps, e->x.p);
-    const GemmArgs up{e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
+    const GemmArgs up{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
     if (c.gelu == MQ_GELU_TANH)
       gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s);
     else
       gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
-    gemm<EPI_RESID>(e, {e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F}, ST_FFN_DOWN, s);
+    gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F}, ST_FFN_DOWN, s);
     e->tl.mark(s, ST_LN);
     hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln2g, w.ln2b,
                        c.ln_eps, e->x.p);
@@ -553,7 +629,8 @@ int mq_encoder_destroy(mq_encoder* e) {
   if (!e) return MQ_OK;
   {
     DeviceGuard dg(e->device);
-    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out}) b->release();
+    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab})
+      b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
   }
@@ -619,12 +696,34 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 3, "bad epi/tile");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 4, "bad epi/tile");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const GemmArgs g{A, K, W, bias, resid, N, out, N, M, N, K};
+  GemmArgs g{nullptr, 0, A, K, W, bias, resid, N, out, N, M, N, K};
   hipStream_t s = (hipStream_t)stream;
+  if (tile == 4) {  // split-K path (test hook: allocates its own slab)
+    MQ_CHECK_ARG(N % 4 == 0, "split-K needs N %% 4 == 0");
+    const int slices = K / kBK;
+    int S = 1;
+    for (int c = 2; c <= slices && c <= 64; ++c)
+      if (slices % c == 0) S = c;
+    float* slab = nullptr;
+    if (hipMalloc((void**)&slab, (size_t)S * M * N * 4) != hipSuccess)
+      MQ_FAIL(MQ_ENOMEM, "slab allocation failed");
+    g.slab = slab;
+    g.slab_floats = (size_t)S * M * N;
+    switch (epi) {
+      case EPI_BIAS: launch_splitk<EPI_BIAS>(g, S, s); break;
+      case EPI_GELU_ERF: launch_splitk<EPI_GELU_ERF>(g, S, s); break;
+      case EPI_GELU_TANH: launch_splitk<EPI_GELU_TANH>(g, S, s); break;
+      default: launch_splitk<EPI_RESID>(g, S, s); break;
+    }
+    const hipError_t err = hipStreamSynchronize(s);
+    (void)hipFree(slab);
+    if (err != hipSuccess) MQ_FAIL(MQ_EHIP, "split-K GEMM failed: %s", hipGetErrorString(err));
+    return MQ_OK;
+  }
   switch (epi) {
     case EPI_BIAS: launch_gemm_tile<EPI_BIAS>(g, tile, cus, s); break;
     case EPI_GELU_ERF: launch_gemm_tile<EPI_GELU_ERF>(g, tile, cus, s); break;
@@ -671,6 +770,9 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   const size_t M = (size_t)B * L;
   if (e->tl.used > 4096) e->tl.drain();  // bound the event pool while timing
   int rc = MQ_OK;
+  // split-K slabs: up to 2*CUs partial tiles of 32 x 128 floats
+  rc = e->slab.ensure((size_t)2 * e->num_cus * 32 * 128);
+  if (rc) return rc;
   for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, M * c.hidden),
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
                   std::make_pair(&e->ffn, M * c.ffn)}) {

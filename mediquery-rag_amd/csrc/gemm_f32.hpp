@@ -39,36 +39,29 @@ struct F32Tile {
 };
 
 // One K-slice of both operands, held in registers between the global load and the
-// LDS write (T14 "issue early / write late").  Row pointers are resolved once per
-// tile (`bind`).  Rows past M / N are clamped onto the last valid row instead of being
-// zeroed: an MFMA output element depends only on its own A row and B row, so the
-// garbage lands only in output rows / columns the epilogue never stores.  The per-slice
-// path is therefore LOADS x global_load_dwordx4 and nothing else.
+// LDS write (T14 "issue early / write late").  Rows past M / N are clamped onto the
+// last valid row instead of being zeroed: an MFMA output element depends only on its
+// own A row and B row, so the garbage lands only in output rows / columns the
+// epilogue never stores.  The per-slice path is LOADS x global_load_dwordx4.
 template <class T>
 struct Stager {
   floatx4 r[T::LOADS];
-  const float* src[T::LOADS];
 
-  __device__ __forceinline__ void bind(const float* __restrict__ A, int64_t lda, int M, int m0,
+  __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda, int M, int m0,
                                        const float* __restrict__ B, int64_t ldb, int64_t N,
-                                       int64_t n0, int tid) {
+                                       int64_t n0, int k0, int tid) {
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
       const int row = f >> 3, ch = f & 7;
+      const float* p;
       if (i < T::BM / 32) {  // compile-time after unrolling: rows [32i, 32i+32) are A rows
-        const int gm = min(m0 + row, M - 1);
-        src[i] = A + (int64_t)gm * lda + ch * 4;
+        p = A + (int64_t)min(m0 + row, M - 1) * lda;
       } else {
-        const int64_t gn = min(n0 + (row - T::BM), N - 1);
-        src[i] = B + gn * ldb + ch * 4;
+        p = B + min(n0 + (int64_t)(row - T::BM), N - 1) * ldb;
       }
+      r[i] = *reinterpret_cast<const floatx4*>(p + k0 + ch * 4);
     }
-  }
-
-  __device__ __forceinline__ void load(int k0) {
-#pragma unroll
-    for (int i = 0; i < T::LOADS; ++i) r[i] = *reinterpret_cast<const floatx4*>(src[i] + k0);
   }
 
   __device__ __forceinline__ void store(float* stage, int tid) const {
@@ -129,6 +122,67 @@ __device__ __forceinline__ int acc_row(int tm, int e, int lane) {
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+// Operands of a tile walk: A [M][lda], B [N][ldb], both K-contiguous, K % 32 == 0.
+struct TileOperands {
+  const float* A;
+  int64_t lda;
+  int M;
+  const float* B;
+  int64_t ldb;
+  int64_t N;
+  int K;
+};
+
+// Stream every K-slice of this workgroup's tiles through a double-buffered LDS image
+// with global loads running TWO slices ahead (two named register stages, so no runtime
+// register indexing): slice j+2 is requested while slice j is multiplied, and slice
+// j+1 - requested one whole slice earlier - is written to the free buffer after the
+// MFMAs.  The prefetch runs straight across tile boundaries.  coords(i, &m0, &n0)
+// gives the origin of the i-th tile; epi(i, acc, released_stage) runs after the last
+// slice of tile i, with `released_stage` an LDS buffer no wave reads until the next
+// barrier the epilogue itself must end with if it uses it.
+template <class T, class Coords, class Epi>
+__device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOperands& op,
+                                           Coords coords, Epi epi) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  const int nk = op.K / kBK;
+  const int S = n_tiles * nk;
+  if (S == 0) return;
+  auto fetch = [&](Stager<T>& st, int j) {
+    const int i = j / nk, kt = j - (j / nk) * nk;
+    int m0;
+    int64_t n0;
+    coords(i, m0, n0);
+    st.load(op.A, op.lda, op.M, m0, op.B, op.ldb, op.N, n0, kt * kBK, tid);
+  };
+  floatx16 acc[T::TM][T::TN];
+  Stager<T> ra, rb;
+  fetch(ra, 0);
+  if (S > 1) fetch(rb, 1);
+  ra.store(lds, tid);
+  __syncthreads();
+  float* buf0 = lds;
+  float* buf1 = lds + T::STAGE_FLOATS;
+  for (int j = 0; j < S; j += 2) {
+    // even half: slice j in buf0, slice j+1 in flight in rb
+    if (j % nk == 0) zero_acc<T>(acc);
+    if (j + 2 < S) fetch(ra, j + 2);
+    mma_slice<T>(buf0, acc, wm, wn, lane);
+    if (j + 1 < S) rb.store(buf1, tid);
+    __syncthreads();
+    if ((j + 1) % nk == 0) epi(j / nk, acc, buf0);
+    if (j + 1 >= S) break;
+    // odd half: slice j+1 in buf1, slice j+2 in flight in ra
+    if ((j + 1) % nk == 0) zero_acc<T>(acc);
+    if (j + 3 < S) fetch(rb, j + 3);
+    mma_slice<T>(buf1, acc, wm, wn, lane);
+    if (j + 2 < S) ra.store(buf0, tid);
+    __syncthreads();
+    if ((j + 2) % nk == 0) epi((j + 1) / nk, acc, buf1);
+  }
 }
 
 }  // namespace mq

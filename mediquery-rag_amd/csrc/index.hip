@@ -121,62 +121,43 @@ __global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
   const int qt = slot % nqt, g = (slot / nqt) * 8 + xcd;
   const int m0 = qt * T::BM;
   const int64_t ntiles = (n_rows + T::BN - 1) / T::BN;
-  const int nk = dim / kBK;
   const int q_local = lane % T::WM, part = lane / T::WM;
 
   TopList<KC> top;
   top.init();
 
-  int64_t t = g;
-  if (t < ntiles) {
-    Stager<T> st;
-    st.bind(Q, dim, nq, m0, C, dim, n_rows, t * T::BN, tid);
-    st.load(0);
-    st.store(lds, tid);
-    __syncthreads();
-    int buf = 0;
-    floatx16 acc[T::TM][T::TN];
-    while (true) {
-      zero_acc<T>(acc);
-      for (int kt = 0; kt < nk; ++kt) {
-        // prefetch the next slice: (t, kt+1) or the first slice of the next row tile
-        const bool same = kt + 1 < nk;
-        const bool more = same || t + G < ntiles;
-        if (!same && more) st.bind(Q, dim, nq, m0, C, dim, n_rows, (t + G) * T::BN, tid);
-        if (more) st.load(same ? (kt + 1) * kBK : 0);
-        mma_slice<T>(lds + buf * T::STAGE_FLOATS, acc, wm, wn, lane);
-        if (more) st.store(lds + (buf ^ 1) * T::STAGE_FLOATS, tid);
-        __syncthreads();
-        buf ^= 1;
-      }
-      // ---- epilogue in the released stage buffer: per wave [WM][32] per pass
-      float* score = lds + (buf ^ 1) * T::STAGE_FLOATS + wave * S::SCORE_FLOATS;
-      const int64_t col0 = t * T::BN + wn * T::WN;
+  const int n_tiles = g < ntiles ? (int)((ntiles - g + G - 1) / G) : 0;
+  auto coords = [&](int i, int& mm0, int64_t& n0) {
+    mm0 = m0;
+    n0 = (g + (int64_t)i * G) * T::BN;
+  };
+  // accumulator -> released stage buffer [WM][32] per wave per pass -> row scans
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
+    float* score = stage + wave * S::SCORE_FLOATS;
+    const int64_t col0 = (g + (int64_t)i * G) * T::BN + wn * T::WN;
 #pragma unroll
-      for (int tn2 = 0; tn2 < T::TN; ++tn2) {
+    for (int tn2 = 0; tn2 < T::TN; ++tn2) {
 #pragma unroll
-        for (int tm = 0; tm < T::TM; ++tm)
+      for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
-          for (int e = 0; e < 16; ++e)
-            score[acc_row(tm, e, lane) * S::SCORE_STRIDE + (lane & 31)] = acc[tm][tn2][e];
-        __syncthreads();
-        const float* row = score + q_local * S::SCORE_STRIDE + part * S::COLS;
-        const int64_t c0 = col0 + tn2 * 32 + part * S::COLS;
+        for (int e = 0; e < 16; ++e)
+          score[acc_row(tm, e, lane) * S::SCORE_STRIDE + (lane & 31)] = acc[tm][tn2][e];
+      __syncthreads();
+      const float* row = score + q_local * S::SCORE_STRIDE + part * S::COLS;
+      const int64_t c0 = col0 + tn2 * 32 + part * S::COLS;
 #pragma unroll
-        for (int c4 = 0; c4 < S::COLS; c4 += 4) {
-          const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
+      for (int c4 = 0; c4 < S::COLS; c4 += 4) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int64_t col = c0 + c4 + e;
-            if (col < n_rows && top.beats_tail(v[e], (int)col)) top.insert(v[e], (int)col);
-          }
+        for (int e = 0; e < 4; ++e) {
+          const int64_t col = c0 + c4 + e;
+          if (col < n_rows && top.beats_tail(v[e], (int)col)) top.insert(v[e], (int)col);
         }
-        __syncthreads();
       }
-      t += G;
-      if (t >= ntiles) break;
+      __syncthreads();
     }
-  }
+  };
+  walk_tiles<T>(lds, n_tiles, TileOperands{Q, dim, nq, C, dim, n_rows, dim}, coords, epi);
 
   const int list = (g * T::WAVES_N + wn) * S::LPQ + part;
   const int qg = m0 + wm * T::WM + q_local;

@@ -27,10 +27,10 @@ def torch_erf(x):
     return torch.erf(x)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(1, 768, 768), (77, 96, 64), (300, 2304, 768),
-                                   (1000, 768, 3072), (4099, 200, 32)])
+                                   (1000, 768, 3072), (4099, 200, 32), (32, 3072, 768), (256, 768, 3072)])
 def test_gemm(require_gpu, tile, epi, M, N, K):
     import torch
     dev = torch.device("cuda", 0)
