@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--layers", type=int, default=DMETA_BASE.layers)
     p.add_argument("--single-iters", type=int, default=50, help="single-query latency samples")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--precision", choices=["f32", "f32x6"], default="f32",
+                   help="GEMM arithmetic: exact f32 MFMA, or fp32 split into 3 bf16 pieces (6 MFMAs)")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     return p.parse_args()
 
@@ -106,6 +108,10 @@ def main():
     index = FlatIndex(dim=768, capacity=cnt, device=local)
     index.add_device(full[off:off + cnt].contiguous())
     enc = Encoder(cfg, device=local)
+    from mediquery_hip import _lib
+    prec = _lib.MQ_DTYPE_F32X6 if args.precision == "f32x6" else _lib.MQ_DTYPE_F32
+    enc.set_precision(prec)
+    index.set_precision(prec)
     ids_np, mask_np = synth.token_batch(B, L, seed=synth.TOKEN_SEED + rank)
     ids = torch.from_numpy(ids_np).to(dev)
     mask = torch.from_numpy(mask_np).to(dev)
@@ -235,7 +241,7 @@ def main():
         "metric": "queries/s (embed+top-k, k=5, b=256) over 1M×768 corpus; p50 single-query ms",
         "value": round(value, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "f32" else "f32 (3xbf16 split, 6 MFMAs)",
         "data": "synthetic (seeded corpus on device, seeded token ids, seeded BERT-base weights)",
         "config": {"workload": "BASELINE config 3: %d x 768 fp32 corpus, batch %d/GPU (L=%d) "
                                "embed + exact top-%d" % (args.corpus_rows, B, L, K),

@@ -42,8 +42,10 @@ extern "C" {
 #define MQ_EIO -4      /* file I/O error (save/load)         */
 #define MQ_ESTATE -5   /* handle in the wrong state          */
 
-#define MQ_DTYPE_F32 0
-#define MQ_DTYPE_BF16 1
+#define MQ_DTYPE_F32 0    /* exact fp32 MFMA (v_mfma_f32_32x32x2_f32)                     */
+#define MQ_DTYPE_BF16 1   /* bf16 storage (coarse paths)                                    */
+#define MQ_DTYPE_F32X6 2  /* fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMAs per
+                           * product, fp32 accumulate: fp32-class error, 2.67x the MFMA rate */
 
 #define MQ_GELU_ERF 0  /* exact erf GELU (HF BERT "gelu")            */
 #define MQ_GELU_TANH 1 /* tanh approximation (ggml / llama.cpp gelu)  */
@@ -82,6 +84,9 @@ int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
                     float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
 /* Copy stored (normalised) rows [row0, row0 + n) into out [n, dim] f32 (host or device). */
 int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device, void* stream);
+/* Arithmetic of the fused scan for large query batches: MQ_DTYPE_F32 (default) or
+ * MQ_DTYPE_F32X6.  Small batches always use the exact f32 kernel (HBM-bound there). */
+int mq_index_set_precision(mq_index* ix, int dtype);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
 /* Device-time accounting with HIP events on the launch stream (off by default).
@@ -123,7 +128,7 @@ int mq_encoder_destroy(mq_encoder* enc);
 int64_t mq_encoder_weight_count(const mq_bert_config* cfg);
 /* Upload the fp32 weight blob (host pointer, n_floats values). */
 int mq_encoder_load_weights(mq_encoder* enc, const float* blob, int64_t n_floats);
-/* Compute dtype of the GEMMs: MQ_DTYPE_F32 (exact fp32 MFMA, default) or MQ_DTYPE_BF16. */
+/* Arithmetic of the GEMMs: MQ_DTYPE_F32 (exact fp32 MFMA, default) or MQ_DTYPE_F32X6. */
 int mq_encoder_set_precision(mq_encoder* enc, int dtype);
 /* Device-time accounting per kernel class (HIP events on the launch stream, off by
  * default).  read_timing returns ms since the last read for the stages
@@ -141,7 +146,8 @@ int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, i
 /* One encoder GEMM on device buffers: out[M,N] = epi(A[M,K] W[N,K]^T + bias (+ resid)),
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,
  * 1 = 128x96, 2 = 128x64, 3 = 32x128, 4 = split-K (32x128 tiles + ordered slab
- * reduction; synchronous, N % 4 == 0).  K % 32 == 0.  For kernel unit tests. */
+ * reduction; synchronous, N % 4 == 0), 5-9 = LDS-DMA variants, 10-12 = split-f32 (x6)
+ * 128x128 / 128x96 / 128x64.  K % 32 == 0.  For kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
 

@@ -21,6 +21,7 @@
 
 #include "common.hpp"
 #include "gemm_f32.hpp"
+#include "gemm_glds.hpp"
 
 namespace mq {
 
@@ -91,6 +92,52 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     }
   };
   walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
+}
+
+// Same GEMM on the LDS-DMA core (gemm_glds.hpp): NS-stage ring, no staging VGPRs.
+template <class T, int EPI>
+__global__ __launch_bounds__(T::THREADS, T::BLOCKS_PER_CU * T::WAVES / 4) void gemm_dma_kernel(
+    const float* __restrict__ A, int lda, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ resid, int ldr,
+    float* __restrict__ out, int ldo, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) float lds[T::LDS_FLOATS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  const int tiles_n = (N + T::BN - 1) / T::BN;
+  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
+  const int G = gridDim.x, per_xcd = G >> 3;
+  const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
+  auto coords = [&](int i, int& m0, int64_t& n0) {
+    const int t = i * G + xslot;
+    m0 = (t / tiles_n) * T::BM;
+    n0 = (int64_t)(t % tiles_n) * T::BN;
+  };
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
+    int m0;
+    int64_t n0l;
+    coords(i, m0, n0l);
+    const int n0 = (int)n0l;
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn) {
+      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float b = bias[col];
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
+          if (row >= M) continue;
+          float v = acc[tm][tn][e] + b;
+          if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+          if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+          if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+          out[(int64_t)row * ldo + col] = v;
+        }
+    }
+  };
+  walk_tiles_dma<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
 }
 
 // ---------------------------------------------------------- split-K GEMM ------
@@ -442,8 +489,43 @@ using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few rows)
 // so a grid that is not a multiple of 2*CUs idles part of the chip in its last round
 // (M = 8192: N = 768 -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost model:
 // rounds * tile area / relative tile efficiency.
+template <class T, int EPI>
+void launch_gemm_dma(const GemmArgs& g, int num_cus, hipStream_t s) {
+  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+  const int grid = (std::min(tiles, T::BLOCKS_PER_CU * num_cus) + 7) / 8 * 8;
+  hipLaunchKernelGGL((gemm_dma_kernel<T, EPI>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda,
+                     g.W, g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
+}
+
+using DmaA = GTile<2, 2, 2, 2, 2>;  // 128x128, 4 waves, 2 stages  (2 / CU)
+using DmaB = GTile<2, 2, 2, 2, 3>;  // 128x128, 4 waves, 3 stages  (1 / CU)
+using DmaC = GTile<4, 1, 1, 3, 2>;  // 128x96,  4 waves, 2 stages  (2 / CU)
+using DmaD = GTile<4, 2, 2, 2, 3>;  // 256x128, 8 waves, 3 stages  (1 / CU)
+using DmaE = GTile<2, 4, 2, 1, 3>;  // 128x128, 8 waves (64x32), 3 stages (1 / CU)
+
+using X6Big = F32Tile<2, 2, 2, 2, true>;  // 128 x 128, split-f32
+using X6T96 = F32Tile<4, 1, 1, 3, true>;  // 128 x 96
+using X6Mid = F32Tile<2, 2, 2, 1, true>;  // 128 x 64
+
 template <int EPI>
 void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
+  switch (tile) {
+    case 10: launch_gemm_t<X6Big, EPI>(g, num_cus, s); return;
+    case 11: launch_gemm_t<X6T96, EPI>(g, num_cus, s); return;
+    case 12: launch_gemm_t<X6Mid, EPI>(g, num_cus, s); return;
+    case 13: launch_gemm_t<F32Tile<2, 2, 2, 2, true, 3>, EPI>(g, num_cus, s); return;
+    case 14: launch_gemm_t<F32Tile<2, 2, 2, 2, true, 4>, EPI>(g, num_cus, s); return;
+    case 15: launch_gemm_t<F32Tile<4, 1, 1, 3, true, 3>, EPI>(g, num_cus, s); return;
+    case 16: launch_gemm_t<F32Tile<4, 1, 1, 3, true, 4>, EPI>(g, num_cus, s); return;
+    case 17: launch_gemm_t<F32Tile<4, 1, 1, 3, false, 3>, EPI>(g, num_cus, s); return;
+    case 18: launch_gemm_t<F32Tile<2, 2, 2, 2, false, 3>, EPI>(g, num_cus, s); return;
+    case 5: launch_gemm_dma<DmaA, EPI>(g, num_cus, s); return;
+    case 6: launch_gemm_dma<DmaB, EPI>(g, num_cus, s); return;
+    case 7: launch_gemm_dma<DmaC, EPI>(g, num_cus, s); return;
+    case 8: launch_gemm_dma<DmaD, EPI>(g, num_cus, s); return;
+    case 9: launch_gemm_dma<DmaE, EPI>(g, num_cus, s); return;
+    default: break;
+  }
   switch (tile) {
     case 0: launch_gemm_t<GemmBig, EPI>(g, num_cus, s); break;
     case 1: launch_gemm_t<GemmT96, EPI>(g, num_cus, s); break;
@@ -478,10 +560,27 @@ void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
 }
 
 template <int EPI>
-void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s) {
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false) {
   const int S = splitk_factor(g, num_cus);
   if (S) {
     launch_splitk<EPI>(g, S, s);
+    return;
+  }
+  if (x6) {  // split-f32 tiles: same waste model over 128x{128,96,64}
+    const int bns[3] = {128, 96, 64};
+    const double effs[3] = {1.0, 0.96, 0.9};
+    const int64_t slots = 2 * (int64_t)num_cus;
+    int best = 0;
+    double best_cost = 1e300;
+    for (int i = 0; i < 3; ++i) {
+      const int64_t tiles = (int64_t)((g.M + 127) / 128) * ((g.N + bns[i] - 1) / bns[i]);
+      const double cost = (double)((tiles + slots - 1) / slots) * 128 * bns[i] / effs[i];
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = i;
+      }
+    }
+    launch_gemm_tile<EPI>(g, 10 + best, num_cus, s);
     return;
   }
   struct Cand {
@@ -532,7 +631,7 @@ namespace {
 template <int EPI>
 void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s);
+  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6);
 }
 
 // One forward.  With CLS pooling the last layer only needs the CLS rows after its
@@ -686,7 +785,9 @@ int mq_encoder_load_weights(mq_encoder* e, const float* blob, int64_t n_floats) 
 int mq_encoder_set_precision(mq_encoder* e, int dtype) {
   clear_error();
   MQ_CHECK_ARG(e, "NULL encoder");
-  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32, "only the f32 encoder path is implemented (got %d)", dtype);
+  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6,
+               "encoder precision must be MQ_DTYPE_F32 or MQ_DTYPE_F32X6 (got %d)", dtype);
+  std::lock_guard<std::mutex> lk(e->mu);
   e->precision = dtype;
   return MQ_OK;
 }
@@ -696,7 +797,7 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 4, "bad epi/tile");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 18, "bad epi/tile");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

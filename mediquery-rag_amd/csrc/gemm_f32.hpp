@@ -1,42 +1,82 @@
-// gemm_f32.hpp - exact-fp32 MFMA tile core for gfx950 (v_mfma_f32_32x32x2_f32).
+// gemm_f32.hpp - fp32 MFMA tile core for gfx950.
 //
 // Computes D[i][j] = sum_k A[i][k] * B[j][k] for a BM x BN block tile, both operands
-// K-contiguous ("NT": activations/queries [M][K], weights/corpus rows [N][K]).
+// K-contiguous ("NT": activations/queries [M][K], weights/corpus rows [N][K]), fp32 in
+// HBM.  Two arithmetic variants share the tile walk:
+//
+//  * exact f32 (X6 = false): v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain (gfx950 has
+//    no xf32).  K is staged in 32-wide slices through a double-buffered LDS image
+//    [rows][36] floats (144-B rows: conflict-free ds_write_b128 / ds_read_b128,
+//    slot = 9*row + 4*h + q mod 16).  MFMA step (q, s), lane half h carries
+//    k = 16h + 4q + s for BOTH operands, so a lane reads 16 contiguous floats per slice.
+//  * split f32 (X6 = true): every fp32 operand is split EXACTLY into three bf16 pieces
+//    x = x0 + x1 + x2 (8 + 8 + 8 significant bits, round-to-nearest at each step) while
+//    it is staged, and each product uses the six bf16 MFMAs (v_mfma_f32_32x32x16_bf16)
+//    x0y0, x0y1, x1y0, x0y2, x1y1, x2y0 with fp32 accumulation: every bf16 x bf16
+//    product is exact in fp32 and the dropped terms x1y2 + x2y1 + x2y2 are < 3 * 2^-24
+//    relative, i.e. fp32-class results at 16/6 = 2.67x the f32 MFMA rate.  K is staged
+//    in 16-wide slices; an LDS row holds the three planes [3][16] bf16 + 16 B pad
+//    (112-B rows: slot = 7*row + 2*plane + h mod 16, conflict-free); lane half h carries
+//    k = 8h + j.
 //
 //  * 256 threads = 4 waves laid out WAVES_M x WAVES_N; each wave owns TM x TN MFMA
 //    tiles of 32x32 (f32x16 accumulators, 16 regs/lane each).
-//  * K is staged in BK = 32 slices through a double-buffered LDS image
-//    [rows][BK + 4] floats: rows of 144 B keep the staging ds_write_b128 and the
-//    fragment ds_read_b128 bank-conflict free (slot = 9*row + 4*h + q mod 16).
-//  * K order inside a slice is permuted so that one lane's 16 k-values are contiguous:
-//    MFMA step (q, s), lane half h (= lane >> 5) carries k = 16h + 4q + s for BOTH
-//    operands, so each lane fetches its fragment with 4 ds_read_b128 per slice
-//    instead of 16 ds_read_b32.  A dot product is order-free up to fp32 rounding, and
-//    the f32 MFMA is an exact fmaf chain (no TF32 / xf32 on gfx950).
-//  * Next-slice global loads are issued into registers before the MFMAs of the current
-//    slice and written to the other LDS buffer after them: one barrier per slice.
+//  * Global loads run two slices ahead in two named register stages (walk_tiles).
 #pragma once
 
 #include "common.hpp"
 
 namespace mq {
 
-constexpr int kBK = 32;
-constexpr int kLdsStride = kBK + 4;  // floats per staged row (144 B)
+constexpr int kBK = 32;              // K granularity every caller must respect
+constexpr int kLdsStride = kBK + 4;  // floats per staged row of the exact-f32 image (144 B)
 
-template <int WAVES_M_, int WAVES_N_, int TM_, int TN_>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+
+template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2>
 struct F32Tile {
   static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
+  static constexpr bool X6 = X6_;
+  static constexpr int PF = PF_;  // register prefetch depth in slices (walk_tiles D)
   static constexpr int WM = TM * 32, WN = TN * 32;  // wave tile
   static constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   static constexpr int THREADS = WAVES_M * WAVES_N * kWave;
   static constexpr int ROWS = BM + BN;
-  static constexpr int LOADS = ROWS * (kBK / 4) / THREADS;  // float4 per thread per slice
-  static constexpr int STAGE_FLOATS = ROWS * kLdsStride;
+  static constexpr int BK = X6 ? 16 : 32;                 // K per staged slice
+  static constexpr int F4_PER_ROW = BK / 4;               // float4 per row per slice
+  static constexpr int ROW_FLOATS = X6 ? 28 : kLdsStride; // LDS row stride in 4-B words
+  static constexpr int TOTAL_F4 = ROWS * F4_PER_ROW;                  // float4 per slice
+  static constexpr int LOADS = (TOTAL_F4 + THREADS - 1) / THREADS;      // per thread
+  static constexpr bool PARTIAL = TOTAL_F4 % THREADS != 0;              // last slot ragged
+  static constexpr int STAGE_FLOATS = ROWS * ROW_FLOATS;
   static_assert(THREADS == 256, "tile core assumes 256-thread workgroups");
   static_assert(BM % 32 == 0 && BN % 32 == 0, "block tile must be a multiple of 32");
-  static_assert(ROWS * (kBK / 4) % THREADS == 0, "staging must divide evenly");
+  static_assert((BM * F4_PER_ROW) % THREADS == 0, "A / B rows must not share a load slot");
 };
+
+// Exact 3-way bf16 split of 4 floats: returns plane p as 4 packed bf16 (2 dwords).
+__device__ __forceinline__ unsigned pk_bf16(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ __forceinline__ float bf16_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+__device__ __forceinline__ void split3(floatx4 x, uint2 (&pl)[3]) {
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const unsigned a = pk_bf16(x.x, x.y), b = pk_bf16(x.z, x.w);
+    pl[p] = make_uint2(a, b);
+    if (p < 2) {  // residual is exact in fp32
+      x.x -= bf16_lo(a);
+      x.y -= bf16_hi(a);
+      x.z -= bf16_lo(b);
+      x.w -= bf16_hi(b);
+    }
+  }
+}
 
 // One K-slice of both operands, held in registers between the global load and the
 // LDS write (T14 "issue early / write late").  Rows past M / N are clamped onto the
@@ -53,9 +93,10 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
-      const int row = f >> 3, ch = f & 7;
+      if (T::PARTIAL && i == T::LOADS - 1 && f >= T::TOTAL_F4) break;
+      const int row = f / T::F4_PER_ROW, ch = f % T::F4_PER_ROW;
       const float* p;
-      if (i < T::BM / 32) {  // compile-time after unrolling: rows [32i, 32i+32) are A rows
+      if (i < T::BM * T::F4_PER_ROW / T::THREADS) {  // compile-time: A rows come first
         p = A + (int64_t)min(m0 + row, M - 1) * lda;
       } else {
         p = B + min(n0 + (int64_t)(row - T::BM), N - 1) * ldb;
@@ -68,8 +109,17 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
-      const int row = f >> 3, ch = f & 7;
-      *reinterpret_cast<floatx4*>(stage + row * kLdsStride + ch * 4) = r[i];
+      if (T::PARTIAL && i == T::LOADS - 1 && f >= T::TOTAL_F4) break;
+      const int row = f / T::F4_PER_ROW, ch = f % T::F4_PER_ROW;
+      if constexpr (T::X6) {
+        uint2 pl[3];
+        split3(r[i], pl);
+        char* base = reinterpret_cast<char*>(stage + row * T::ROW_FLOATS) + ch * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * 32) = pl[p];
+      } else {
+        *reinterpret_cast<floatx4*>(stage + row * T::ROW_FLOATS + ch * 4) = r[i];
+      }
     }
   }
 };
@@ -79,17 +129,46 @@ template <class T>
 __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T::TM][T::TN],
                                           int wm, int wn, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  const float* as = stage + (wm * T::WM + r) * kLdsStride + h * 16;
-  const float* bs = stage + (T::BM + wn * T::WN + r) * kLdsStride + h * 16;
+  if constexpr (T::X6) {
+    // lane half h: k = 8h .. 8h+7 of this 16-wide slice, one ds_read_b128 per plane
+    const char* as = reinterpret_cast<const char*>(stage + (wm * T::WM + r) * T::ROW_FLOATS) + h * 16;
+    const char* bs = reinterpret_cast<const char*>(stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS) + h * 16;
+    bf16x8 a[T::TM][3], b[T::TN][3];
+#pragma unroll
+    for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[tm][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uintx4*>(as + tm * 32 * T::ROW_FLOATS * 4 + p * 32));
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        b[tn][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uintx4*>(bs + tn * 32 * T::ROW_FLOATS * 4 + p * 32));
+#pragma unroll
+    for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn) {
+        // smallest terms first
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][2], b[tn][0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][1], b[tn][1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][0], b[tn][2], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][1], b[tn][0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][0], b[tn][1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm][0], b[tn][0], acc[tm][tn], 0, 0, 0);
+      }
+    return;
+  }
+  const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * 16;
+  const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * 16;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     floatx4 a[T::TM], b[T::TN];
 #pragma unroll
     for (int tm = 0; tm < T::TM; ++tm)
-      a[tm] = *reinterpret_cast<const floatx4*>(as + tm * 32 * kLdsStride + q * 4);
+      a[tm] = *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4);
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn)
-      b[tn] = *reinterpret_cast<const floatx4*>(bs + tn * 32 * kLdsStride + q * 4);
+      b[tn] = *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -136,19 +215,33 @@ struct TileOperands {
 };
 
 // Stream every K-slice of this workgroup's tiles through a double-buffered LDS image
-// with global loads running TWO slices ahead (two named register stages, so no runtime
-// register indexing): slice j+2 is requested while slice j is multiplied, and slice
-// j+1 - requested one whole slice earlier - is written to the free buffer after the
-// MFMAs.  The prefetch runs straight across tile boundaries.  coords(i, &m0, &n0)
-// gives the origin of the i-th tile; epi(i, acc, released_stage) runs after the last
-// slice of tile i, with `released_stage` an LDS buffer no wave reads until the next
-// barrier the epilogue itself must end with if it uses it.
-template <class T, class Coords, class Epi>
+// with global loads running D slices ahead in D named register stages (compile-time
+// stage indices: no runtime register indexing).  Iteration j: request slice j+D into
+// the stage slice j vacated, multiply slice j, then write slice j+1 (requested D-1
+// iterations earlier) to the free LDS buffer; one barrier.  The prefetch runs straight
+// across tile boundaries.  coords(i, &m0, &n0) gives the origin of the i-th tile;
+// epi(i, acc, released_stage) runs after the last slice of tile i, with
+// `released_stage` an LDS buffer no wave reads before the next barrier (an epilogue
+// that uses it must end with a barrier).
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <class T, int D = T::PF, class Coords, class Epi>
 __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOperands& op,
                                            Coords coords, Epi epi) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
-  const int nk = op.K / kBK;
+  const int nk = op.K / T::BK;
   const int S = n_tiles * nk;
   if (S == 0) return;
   auto fetch = [&](Stager<T>& st, int j) {
@@ -156,32 +249,33 @@ __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOp
     int m0;
     int64_t n0;
     coords(i, m0, n0);
-    st.load(op.A, op.lda, op.M, m0, op.B, op.ldb, op.N, n0, kt * kBK, tid);
+    st.load(op.A, op.lda, op.M, m0, op.B, op.ldb, op.N, n0, kt * T::BK, tid);
   };
   floatx16 acc[T::TM][T::TN];
-  Stager<T> ra, rb;
-  fetch(ra, 0);
-  if (S > 1) fetch(rb, 1);
-  ra.store(lds, tid);
+  Stager<T> st[D];
+  static_for<D>([&](auto dc) {
+    constexpr int d = decltype(dc)::value;
+    if (d < S) fetch(st[d], d);
+  });
+  st[0].store(lds, tid);
   __syncthreads();
-  float* buf0 = lds;
-  float* buf1 = lds + T::STAGE_FLOATS;
-  for (int j = 0; j < S; j += 2) {
-    // even half: slice j in buf0, slice j+1 in flight in rb
-    if (j % nk == 0) zero_acc<T>(acc);
-    if (j + 2 < S) fetch(ra, j + 2);
-    mma_slice<T>(buf0, acc, wm, wn, lane);
-    if (j + 1 < S) rb.store(buf1, tid);
-    __syncthreads();
-    if ((j + 1) % nk == 0) epi(j / nk, acc, buf0);
-    if (j + 1 >= S) break;
-    // odd half: slice j+1 in buf1, slice j+2 in flight in ra
-    if ((j + 1) % nk == 0) zero_acc<T>(acc);
-    if (j + 3 < S) fetch(rb, j + 3);
-    mma_slice<T>(buf1, acc, wm, wn, lane);
-    if (j + 2 < S) ra.store(buf0, tid);
-    __syncthreads();
-    if ((j + 2) % nk == 0) epi((j + 1) / nk, acc, buf1);
+  for (int j0 = 0; j0 < S; j0 += D) {
+    bool done = false;
+    static_for<D>([&](auto dc) {
+      constexpr int d = decltype(dc)::value;
+      const int j = j0 + d;
+      if (done || j >= S) {
+        done = true;
+        return;
+      }
+      if (j + D < S) fetch(st[d], j + D);  // slice j's stage is free (stored last iteration)
+      if (j % nk == 0) zero_acc<T>(acc);
+      float* cur = lds + (j & 1) * T::STAGE_FLOATS;
+      mma_slice<T>(cur, acc, wm, wn, lane);
+      if (j + 1 < S) st[(d + 1) % D].store(lds + ((j + 1) & 1) * T::STAGE_FLOATS, tid);
+      __syncthreads();
+      if ((j + 1) % nk == 0) epi(j / nk, acc, cur);
+    });
   }
 }
 

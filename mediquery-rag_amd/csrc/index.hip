@@ -84,6 +84,7 @@ struct TopList {
 
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
+using SearchWideX6 = F32Tile<2, 2, 2, 2, true>;  // same, split-f32 arithmetic
 using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
 
 template <class T>
@@ -91,10 +92,12 @@ struct SearchSmem {
   // The finished wave tile is scanned in TN passes of 32 columns; each pass parks the
   // wave's [WM][32] scores in the LDS stage buffer the last K-slice just released
   // (row stride 36 floats = 144 B: conflict-free ds_read_b128 row scans).
-  static constexpr int SCORE_STRIDE = 36;
+  // (exact-f32 stages hold 32-column passes; the smaller split-f32 stages 16-column ones)
+  static constexpr int PASS_COLS = T::X6 ? 16 : 32;
+  static constexpr int SCORE_STRIDE = PASS_COLS + 4;
   static constexpr int SCORE_FLOATS = T::WM * SCORE_STRIDE;  // per wave per pass
   static constexpr int LPQ = kWave / T::WM;                   // lanes scanning one query row
-  static constexpr int COLS = 32 / LPQ;                       // columns per lane per pass
+  static constexpr int COLS = PASS_COLS / LPQ;                // columns per lane per pass
   static_assert(4 * SCORE_FLOATS <= T::STAGE_FLOATS, "score tile must fit a stage buffer");
   static_assert(2 * T::STAGE_FLOATS * 4 <= 80 * 1024, "two workgroups per CU");
 };
@@ -136,15 +139,18 @@ __global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
     float* score = stage + wave * S::SCORE_FLOATS;
     const int64_t col0 = (g + (int64_t)i * G) * T::BN + wn * T::WN;
 #pragma unroll
-    for (int tn2 = 0; tn2 < T::TN; ++tn2) {
+    for (int pass = 0; pass < T::TN * 32 / S::PASS_COLS; ++pass) {
+      const int tn2 = pass * S::PASS_COLS / 32, sub = pass % (32 / S::PASS_COLS);
+      if ((lane & 31) / S::PASS_COLS == sub) {
 #pragma unroll
-      for (int tm = 0; tm < T::TM; ++tm)
+        for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
-        for (int e = 0; e < 16; ++e)
-          score[acc_row(tm, e, lane) * S::SCORE_STRIDE + (lane & 31)] = acc[tm][tn2][e];
+          for (int e = 0; e < 16; ++e)
+            score[acc_row(tm, e, lane) * S::SCORE_STRIDE + (lane & 31) % S::PASS_COLS] = acc[tm][tn2][e];
+      }
       __syncthreads();
       const float* row = score + q_local * S::SCORE_STRIDE + part * S::COLS;
-      const int64_t c0 = col0 + tn2 * 32 + part * S::COLS;
+      const int64_t c0 = col0 + pass * S::PASS_COLS + part * S::COLS;
 #pragma unroll
       for (int c4 = 0; c4 < S::COLS; c4 += 4) {
         const floatx4 v = *reinterpret_cast<const floatx4*>(row + c4);
@@ -308,6 +314,7 @@ struct mq_index {
   int num_cus = 256;
   DevBuf stage, cand_s, cand_i, out_s, out_i;
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
+  int precision = MQ_DTYPE_F32;
   std::mutex mu;
 };
 
@@ -393,7 +400,9 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
   }
   if (ix->tl.used > 4096) ix->tl.drain();
   ix->tl.mark(s, 0);
-  if (p.wide) {
+  if (p.wide && ix->precision == MQ_DTYPE_F32X6) {
+    MQ_SEARCH(SearchWideX6)
+  } else if (p.wide) {
     MQ_SEARCH(SearchWide)
   } else {
     MQ_SEARCH(SearchNarrow)
@@ -581,6 +590,16 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
   MQ_HIP(hipMemcpyAsync(out, ix->rows + row0 * ix->dim, (size_t)n * ix->dim * 4,
                         out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
   if (!out_on_device) MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_index_set_precision(mq_index* ix, int dtype) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6,
+               "search precision must be MQ_DTYPE_F32 or MQ_DTYPE_F32X6 (got %d)", dtype);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->precision = dtype;
   return MQ_OK;
 }
 

@@ -74,6 +74,10 @@ class FlatIndex:
 
     STAGES = ("flat_search_kernel", "merge_kernel")
 
+    def set_precision(self, dtype):
+        """_lib.MQ_DTYPE_F32 (exact f32 MFMA) or _lib.MQ_DTYPE_F32X6 (split-f32)."""
+        _lib.call("mq_index_set_precision", self._h, dtype)
+
     def set_timing(self, enabled=True):
         _lib.call("mq_index_set_timing", self._h, int(bool(enabled)))
 

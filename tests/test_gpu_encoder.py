@@ -27,6 +27,7 @@ def g(golden):
     return np.load(os.path.join(golden, "encoder_golden.npz"))
 
 
+@pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6])
 @pytest.mark.parametrize("case,cfg", [
     ("tiny_a", BertConfig(layers=2)),
     ("tiny_b", BertConfig(layers=2)),
@@ -34,16 +35,18 @@ def g(golden):
     ("tiny_tanh", BertConfig(layers=2, gelu=GELU_TANH)),
     ("base", DMETA_BASE),
 ])
-def test_golden(require_gpu, g, case, cfg):
+def test_golden(require_gpu, g, case, cfg, prec):
     src = case.replace("_mean", "")
     enc = Encoder(cfg)
+    enc.set_precision(prec)
     _close(enc.embed(g[src + "_ids"], g[src + "_mask"]), g[case + "_emb"])
 
 
 @pytest.mark.parametrize("B,L,ragged", [(1, 1, False), (1, 2, False), (3, 31, True), (5, 33, True),
                                         (2, 64, False), (4, 65, True), (9, 130, True),
                                         (2, 300, True), (1, 512, False), (70, 32, False)])
-def test_shapes_vs_oracle(require_gpu, B, L, ragged):
+@pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6])
+def test_shapes_vs_oracle(require_gpu, B, L, ragged, prec):
     cfg = BertConfig(layers=2)
     rng = np.random.default_rng(B * 1000 + L)
     ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
@@ -54,7 +57,9 @@ def test_shapes_vs_oracle(require_gpu, B, L, ragged):
             mask[b, n:] = 0
             ids[b, n:] = 0
     ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
-    _close(Encoder(cfg).embed(ids, mask), ref)
+    enc = Encoder(cfg)
+    enc.set_precision(prec)
+    _close(enc.embed(ids, mask), ref)
 
 
 def test_device_path_and_batch_invariance(require_gpu):

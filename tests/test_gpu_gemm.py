@@ -27,7 +27,7 @@ def torch_erf(x):
     return torch.erf(x)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tile", list(range(19)))
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(1, 768, 768), (77, 96, 64), (300, 2304, 768),
                                    (1000, 768, 3072), (4099, 200, 32), (32, 3072, 768), (256, 768, 3072)])
@@ -47,3 +47,24 @@ def test_gemm(require_gpu, tile, epi, M, N, K):
     err = (out.double() - ref).abs().max().item()
     assert not torch.isnan(out).any()
     assert err < 2e-5 * math.sqrt(K) * 4, err
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (300, 2304, 3072), (1024, 3072, 768)])
+def test_split_f32_is_fp32_class(require_gpu, M, N, K):
+    """The 3-way bf16 split with six MFMAs per product (tile 10) must be as accurate as
+    the exact f32 MFMA (tile 0) against a float64 reference: max error within 3x."""
+    import torch
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(11)
+    A = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.05
+    b = torch.zeros(N, device=dev)
+    ref = A.double() @ W.double().T
+    errs = {}
+    for tile in (0, 10):
+        out = torch.empty(M, N, device=dev)
+        _lib.call("mq_debug_gemm_f32", _lib.ptr(A), _lib.ptr(W), _lib.ptr(b), _lib.ptr(b), _lib.ptr(out),
+                  M, N, K, 0, tile, _lib.stream_handle())
+        torch.cuda.synchronize()
+        errs[tile] = (out.double() - ref).abs().max().item()
+    assert errs[10] <= 3 * errs[0] + 1e-7, errs

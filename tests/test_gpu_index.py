@@ -6,25 +6,30 @@ import os
 import numpy as np
 import pytest
 
-from mediquery_hip import synth
+from mediquery_hip import _lib, synth
 from mediquery_hip.native import FlatIndex, merge_topk_device, merge_topk_host
 from oracle.flat import check_topk, exact_scores, search
 
 pytestmark = pytest.mark.gpu
 
 
-def _index(rows):
+def _index(rows, prec=_lib.MQ_DTYPE_F32):
     ix = FlatIndex(dim=rows.shape[1])
     ix.add(rows)
+    ix.set_precision(prec)
     return ix
 
 
-def test_flat_golden_fixture(require_gpu, golden):
+PRECS = [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6]
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_flat_golden_fixture(require_gpu, golden, prec):
     f = np.load(os.path.join(golden, "flat_golden.npz"))
     c = synth.corpus(int(f["n"]), int(f["dim"]), clustered=True)
     q, planted = synth.queries(int(f["nq"]), c)
     ref = exact_scores(q, c)
-    ix = _index(c)
+    ix = _index(c, prec)
     for k in (5, 50):
         s, i = ix.search(q, k)
         assert check_topk(i, s, ref, k) == [], k
@@ -35,10 +40,11 @@ def test_flat_golden_fixture(require_gpu, golden):
 @pytest.mark.parametrize("n,nq,k", [
     (1, 1, 1), (5, 3, 8), (127, 7, 5), (128, 32, 5), (129, 33, 9), (1000, 64, 32),
     (1000, 65, 33), (4099, 128, 5), (4099, 200, 64), (3000, 256, 5), (700, 1, 64), (2500, 300, 17)])
-def test_shapes_vs_oracle(require_gpu, n, nq, k):
+@pytest.mark.parametrize("prec", PRECS)
+def test_shapes_vs_oracle(require_gpu, n, nq, k, prec):
     c = synth.corpus(n, 768, seed=n)
     q, _ = synth.queries(nq, c, seed=nq)
-    ix = _index(c)
+    ix = _index(c, prec)
     s, i = ix.search(q, k)
     ref = exact_scores(q, c)
     kk = min(k, n)
@@ -120,7 +126,8 @@ def test_device_pointer_path_and_device_merge(require_gpu):
     np.testing.assert_array_equal(di.cpu().numpy(), hi)
 
 
-def test_full_size_1m_planted_and_fp64_reference(require_gpu):
+@pytest.mark.parametrize("prec", PRECS)
+def test_full_size_1m_planted_and_fp64_reference(require_gpu, prec):
     """BASELINE config 3 size (1M x 768, B = 256, k = 5): planted queries hit their
     rows, and the ids equal a float64 torch reference of the same device corpus."""
     import torch
@@ -129,6 +136,7 @@ def test_full_size_1m_planted_and_fp64_reference(require_gpu):
     q, planted = synth.queries_device(256, rows)
     ix = FlatIndex(dim=768, capacity=1_000_000)
     ix.add_device(rows)
+    ix.set_precision(prec)
     s = torch.empty((256, 5), dtype=torch.float32, device=dev)
     i = torch.empty((256, 5), dtype=torch.int64, device=dev)
     ix.search_device(q, 5, s, i)

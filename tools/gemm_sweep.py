@@ -11,7 +11,7 @@ from mediquery_hip import _lib  # noqa: E402
 
 SHAPES = {"qkv": (8192, 2304, 768), "out_proj": (8192, 768, 768), "ffn_up": (8192, 3072, 768),
           "ffn_down": (8192, 768, 3072)}
-TILES = ["128x128", "128x96", "128x64", "32x128"]
+TILES = ["128x128", "128x96", "128x64", "32x128", "splitk", "dmaA_128x128_ns2", "dmaB_128x128_ns3", "dmaC_128x96_ns2", "dmaD_256x128_8w_ns3", "dmaE_128x128_8w_ns3", "x6_128x128", "x6_128x96", "x6_128x64", "x6_128x128_pf3", "x6_128x128_pf4", "x6_128x96_pf3", "x6_128x96_pf4", "f32_128x96_pf3", "f32_128x128_pf3"]
 
 
 def main():
@@ -25,6 +25,8 @@ def main():
         out = torch.empty(M, N, device=dev)
         epi = 1 if name == "ffn_up" else (3 if name in ("out_proj", "ffn_down") else 0)
         for t, tname in enumerate(TILES):
+            if tname == "splitk":
+                continue
             def run():
                 _lib.call("mq_debug_gemm_f32", _lib.ptr(A), _lib.ptr(W), _lib.ptr(b), _lib.ptr(R),
                           _lib.ptr(out), M, N, K, epi, t, _lib.stream_handle())
@@ -40,6 +42,8 @@ def main():
             ms = e0.elapsed_time(e1) / n
             res["%s/%s" % (name, tname)] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
     print(json.dumps(res, indent=1))
+    for k, v in res.items():
+        print("%-32s %6.1f TF" % (k, v["tflops"]))
 
 
 if __name__ == "__main__":
