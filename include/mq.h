@@ -142,6 +142,22 @@ int mq_encoder_read_timing(mq_encoder* enc, float* ms, int n);
 int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, int B, int L,
                      float* out, int io_on_device, void* stream);
 
+/* ------------------------------------------------------------ tokenizer ---- */
+/* Host-side BERT tokenisation (the step Ollama runs before the forward, reference
+ * src/medical_engine.py:43).  WordPiece over a local vocab.txt, or the deterministic
+ * char tokenizer (id = 106 + crc32(char) % (vocab - 106)).  Sequences are
+ * [CLS] body [SEP], truncated to max_length, right-padded with 0. */
+typedef struct mq_tokenizer mq_tokenizer;
+int mq_tokenizer_create_wordpiece(const char* vocab_path, int lower_case, int max_length,
+                                  mq_tokenizer** out);
+int mq_tokenizer_create_char(int vocab_size, int max_length, mq_tokenizer** out);
+int mq_tokenizer_destroy(mq_tokenizer* tok);
+/* Encode n NUL-terminated UTF-8 texts.  ids / mask must hold n * max(max_length, pad_to)
+ * int32; they are written as [n, L] row-major with L = max(longest sequence, pad_to),
+ * returned in *out_len. */
+int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n, int pad_to,
+                              int32_t* ids, int32_t* mask, int* out_len);
+
 /* ------------------------------------------------------- testing hooks ---- */
 /* One encoder GEMM on device buffers: out[M,N] = epi(A[M,K] W[N,K]^T + bias (+ resid)),
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,

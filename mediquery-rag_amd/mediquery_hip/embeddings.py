@@ -16,7 +16,7 @@ import numpy as np
 from .compat import EmbeddingsBase
 from .config import BertConfig, DMETA_BASE
 from .native import Encoder
-from .tokenizer import CharTokenizer, WordPieceTokenizer
+from .tokenizer import NativeTokenizer
 from .weights import load_safetensors
 
 
@@ -39,10 +39,10 @@ class HipBertEmbeddings(EmbeddingsBase):
         self.max_length = min(int(max_length), config.max_positions)
         weights = load_safetensors(weights_path, config) if weights_path else None
         self.encoder = Encoder(config, weights=weights, seed=seed, device=device)
-        if vocab_file:
-            self.tokenizer = WordPieceTokenizer(vocab_file, max_length=self.max_length)
+        if vocab_file:  # C++ tokenizers of libmqhip.so
+            self.tokenizer = NativeTokenizer.wordpiece(vocab_file, max_length=self.max_length)
         else:
-            self.tokenizer = CharTokenizer(config.vocab_size, max_length=self.max_length)
+            self.tokenizer = NativeTokenizer.char(config.vocab_size, max_length=self.max_length)
 
     # ---- batched core -------------------------------------------------------------
     def embed_array(self, texts):
@@ -51,17 +51,14 @@ class HipBertEmbeddings(EmbeddingsBase):
         out = np.empty((len(texts), self.config.hidden), dtype=np.float32)
         if not texts:
             return out
-        seqs = [self.tokenizer.encode(t) for t in texts]
-        order = sorted(range(len(seqs)), key=lambda i: len(seqs[i]))
+        all_ids, all_mask = self.tokenizer(texts)
+        lens = all_mask.sum(1)
+        order = np.argsort(lens, kind="stable")
         for s in range(0, len(order), self.batch_size):
             idx = order[s:s + self.batch_size]
-            L = max(len(seqs[i]) for i in idx)
-            ids = np.zeros((len(idx), L), dtype=np.int32)
-            mask = np.zeros((len(idx), L), dtype=np.int32)
-            for r, i in enumerate(idx):
-                ids[r, :len(seqs[i])] = seqs[i]
-                mask[r, :len(seqs[i])] = 1
-            out[idx] = self.encoder.embed(ids, mask)
+            L = int(lens[idx].max())
+            out[idx] = self.encoder.embed(np.ascontiguousarray(all_ids[idx, :L]),
+                                          np.ascontiguousarray(all_mask[idx, :L]))
         return out
 
     # ---- LangChain Embeddings interface ---------------------------------------------

@@ -9,6 +9,8 @@ not available offline, so two tokenisers are provided:
   id = 106 + crc32(char) mod (vocab - 106), framed by [CLS]=101 / [SEP]=102, [PAD]=0.
 * `WordPieceTokenizer` - BERT basic + greedy longest-match WordPiece over a LOCAL
   vocab.txt, for use with real weights.
+`NativeTokenizer` runs either scheme in C++ inside libmqhip.so (mq_tokenizer_*); the two
+Python classes above are its parity twins (tests/test_tokenizer_native.py).
 """
 import unicodedata
 import zlib
@@ -128,3 +130,59 @@ class WordPieceTokenizer:
 
     def __call__(self, texts, pad_to=None):
         return _pack([self.encode(t) for t in texts], self.max_length, pad_to)
+
+
+class NativeTokenizer:
+    """C++ tokenizer of libmqhip.so: `NativeTokenizer.char(vocab, max_length)` or
+    `NativeTokenizer.wordpiece(vocab_file, max_length, lower_case)`; call like the Python
+    tokenizers: tok(texts, pad_to=None) -> (ids, mask) int32 [n, L]."""
+
+    def __init__(self, handle, max_length):
+        self._h = handle
+        self.max_length = max_length
+
+    @classmethod
+    def char(cls, vocab_size=21128, max_length=512):
+        import ctypes
+        from . import _lib
+        h = ctypes.c_void_p()
+        _lib.call("mq_tokenizer_create_char", vocab_size, max_length, ctypes.byref(h))
+        return cls(h, max_length)
+
+    @classmethod
+    def wordpiece(cls, vocab_file, max_length=512, lower_case=True):
+        import ctypes
+        from . import _lib
+        h = ctypes.c_void_p()
+        _lib.call("mq_tokenizer_create_wordpiece", str(vocab_file).encode(), int(lower_case),
+                  max_length, ctypes.byref(h))
+        return cls(h, max_length)
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            try:
+                from . import _lib
+                _lib.lib().mq_tokenizer_destroy(h)
+            except Exception:
+                pass
+
+    __del__ = close
+
+    def __call__(self, texts, pad_to=None):
+        import ctypes
+        from . import _lib
+        texts = list(texts)
+        n = len(texts)
+        cap = max(self.max_length, pad_to or 0)
+        ids = np.zeros(max(1, n * cap), dtype=np.int32)
+        mask = np.zeros(max(1, n * cap), dtype=np.int32)
+        arr = (ctypes.c_char_p * max(1, n))(*[t.encode("utf-8") for t in texts])
+        L = ctypes.c_int()
+        _lib.call("mq_tokenizer_encode_batch", self._h, arr, n, int(pad_to or 0), _lib.ptr(ids),
+                  _lib.ptr(mask), ctypes.byref(L))
+        return ids[:n * L.value].reshape(n, L.value).copy(), mask[:n * L.value].reshape(n, L.value).copy()
+
+    def encode(self, text):
+        ids, mask = self([text])
+        return ids[0, :int(mask[0].sum())].tolist()
