@@ -98,10 +98,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MQ_DIST_BACKEND=gloo rehearses the N-rank path with several ranks on one GPU
+    backend = os.environ.get("MQ_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     cfg = DMETA_BASE if args.layers == DMETA_BASE.layers else \
         type(DMETA_BASE)(layers=args.layers)
     B, L, K = args.batch, args.seq_len, args.k
@@ -175,7 +181,7 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([elapsed], device=dev)
+            t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         stage_ms = {k: v / args.steps for k, v in enc.read_timing().items()}

@@ -36,12 +36,15 @@ class ShardedSearcher:
     def _all_gather(self, t):
         world = dist.get_world_size(self.group)
         t = t.contiguous()
-        out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         if dist.get_backend(self.group) == "nccl":  # RCCL: one collective into one buffer
+            out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
             dist.all_gather_into_tensor(out, t, group=self.group)
-        else:  # gloo (CPU tests)
-            dist.all_gather(list(out.unbind(0)), t, group=self.group)
-        return out
+            return out
+        # gloo (CPU tests, or several ranks sharing one GPU in a rehearsal): host bounce
+        src = t.cpu()
+        out = torch.empty((world,) + tuple(src.shape), dtype=src.dtype)
+        dist.all_gather(list(out.unbind(0)), src, group=self.group)
+        return out.to(t.device)
 
     def gather_queries(self, q_local):
         """[B, dim] per rank -> [world*B, dim] on every rank (rank-major)."""
