@@ -84,8 +84,11 @@ int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
                     float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
 /* Copy stored (normalised) rows [row0, row0 + n) into out [n, dim] f32 (host or device). */
 int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device, void* stream);
-/* Arithmetic of the fused scan for large query batches: MQ_DTYPE_F32 (default) or
- * MQ_DTYPE_F32X6.  Small batches always use the exact f32 kernel (HBM-bound there). */
+/* Arithmetic of the fused scan: MQ_DTYPE_F32 (default, exact), MQ_DTYPE_F32X6 (split
+ * fp32, large batches; small batches stay on the exact kernel, HBM-bound there), or
+ * MQ_DTYPE_BF16: bf16 shadow slab scanned on bf16 MFMA for the top max(k, 50) (capped
+ * at MQ_MAX_K) candidates, then an exact fp32 re-rank to the top-k (BASELINE config 5;
+ * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0. */
 int mq_index_set_precision(mq_index* ix, int dtype);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);

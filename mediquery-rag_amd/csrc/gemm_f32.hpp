@@ -34,11 +34,17 @@ constexpr int kLdsStride = kBK + 4;  // floats per staged row of the exact-f32 i
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
-template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2>
+template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2,
+          bool BF16_ = false>
 struct F32Tile {
   static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
   static constexpr bool X6 = X6_;
   static constexpr int PF = PF_;  // register prefetch depth in slices (walk_tiles D)
+  // BF16: both operands are bf16 in memory, addressed as float-typed rows of half the
+  // width (two bf16 per 4-byte slot): the staging is byte-identical to the f32 path and
+  // a 32-slot slice carries 64 k-values; only the MFMA (32x32x16 bf16) differs.
+  static constexpr bool BF16 = BF16_;
+  static_assert(!(X6 && BF16), "one arithmetic mode");
   static constexpr int WM = TM * 32, WN = TN * 32;  // wave tile
   static constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   static constexpr int THREADS = WAVES_M * WAVES_N * kWave;
@@ -129,6 +135,27 @@ template <class T>
 __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T::TM][T::TN],
                                           int wm, int wn, int lane) {
   const int r = lane & 31, h = lane >> 5;
+  if constexpr (T::BF16) {
+    // lane half h: k = 32h .. 32h+31 of the 64-wide slice; step q takes k = 32h + 8q + j
+    const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * 16;
+    const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bf16x8 a[T::TM], b[T::TN];
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+        a[tm] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4));
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn)
+        b[tn] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4));
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
+    }
+    return;
+  }
   if constexpr (T::X6) {
     // lane half h: k = 8h .. 8h+7 of this 16-wide slice, one ds_read_b128 per plane
     const char* as = reinterpret_cast<const char*>(stage + (wm * T::WM + r) * T::ROW_FLOATS) + h * 16;

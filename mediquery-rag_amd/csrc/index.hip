@@ -85,6 +85,8 @@ struct TopList {
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
 using SearchWideX6 = F32Tile<2, 2, 2, 2, true>;  // same, split-f32 arithmetic
+using SearchWideBF = F32Tile<2, 2, 2, 2, false, 2, true>;    // bf16 coarse scan
+using SearchNarrowBF = F32Tile<1, 4, 1, 1, false, 2, true>;  // bf16 coarse, small batches
 using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
 
 template <class T>
@@ -103,15 +105,16 @@ struct SearchSmem {
 };
 
 // Grid: nqt query tiles x G row groups (G % 8 == 0).  Block (qt, g) scans row tiles
-// g, g+G, g+2G, ... for queries [qt*BM, qt*BM + BM) and leaves, per lane, the top-k of
-// what it saw in cand[list][query][0..k) with list = (g*WAVES_N + wn)*LPQ + part.
+// g, g+G, g+2G, ... for queries [qt*BM, qt*BM + BM) and leaves, per lane, the best
+// kl (<= KC) of what it saw in cand[list][query][0..kl) with
+// list = (g*WAVES_N + wn)*LPQ + part.
 // Scores never leave the chip: each finished tile goes accumulator -> LDS (the stage
 // buffer the last slice released) -> one lane per (query, part) scans its row against
 // its register top-KC list; only beating the list tail costs an insertion.
 template <class T, int KC>
-__global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
+__global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
     const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
-    int G, int nqt, int k, float* __restrict__ cand_s, int* __restrict__ cand_i) {
+    int G, int nqt, int kl, float* __restrict__ cand_s, int* __restrict__ cand_i) {
   using S = SearchSmem<T>;
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
 
@@ -130,12 +133,14 @@ __global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
   top.init();
 
   const int n_tiles = g < ntiles ? (int)((ntiles - g + G - 1) / G) : 0;
-  auto coords = [&](int i, int& mm0, int64_t& n0) {
+  auto coords = [&](int i, int& mm0, int64_t& n0) __attribute__((always_inline)) {
     mm0 = m0;
     n0 = (g + (int64_t)i * G) * T::BN;
   };
   // accumulator -> released stage buffer [WM][32] per wave per pass -> row scans
-  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
+  // (always_inline: an outlined epilogue would take `top` and `acc` by address and
+  // put both in scratch)
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) __attribute__((always_inline)) {
     float* score = stage + wave * S::SCORE_FLOATS;
     const int64_t col0 = (g + (int64_t)i * G) * T::BN + wn * T::WN;
 #pragma unroll
@@ -168,28 +173,89 @@ __global__ __launch_bounds__(256, KC <= 8 ? 2 : 1) void flat_search_kernel(
   const int list = (g * T::WAVES_N + wn) * S::LPQ + part;
   const int qg = m0 + wm * T::WM + q_local;
   if (qg < nq) {
-    const int64_t base = ((int64_t)list * nq + qg) * k;
+    const int64_t base = ((int64_t)list * nq + qg) * kl;
 #pragma unroll
     for (int i = 0; i < KC; ++i)
-      if (i < k) {
+      if (i < kl) {
         cand_s[base + i] = top.s[i];
         cand_i[base + i] = top.id[i];
       }
   }
 }
 
+// ================================================= bf16 coarse path (config 5) ==
+// fp32 -> bf16 (round to nearest even), two elements per thread.
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ src,
+                                                      unsigned* __restrict__ dst, int64_t n_pairs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_pairs) return;
+  const float2 v = reinterpret_cast<const float2*>(src)[i];
+  dst[i] = pk_bf16(v.x, v.y);
+}
+
+// Exact fp32 re-rank of the coarse candidates: one block per query, one wave per
+// candidate dot product (768-wide, float4 per lane), then every candidate's rank by
+// (score desc, id asc) picks its output slot.
+__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q,
+                                                     const float* __restrict__ rows, int dim,
+                                                     const int64_t* __restrict__ cand, int kc,
+                                                     int k, float* __restrict__ out_s,
+                                                     int64_t* __restrict__ out_i) {
+  __shared__ float sc[MQ_MAX_K];
+  __shared__ long long sid[MQ_MAX_K];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
+  for (int c = wave; c < kc; c += 4) {
+    const long long id = cand[q * kc + c];
+    float acc = 0.f;
+    if (id >= 0) {
+      const floatx4* r4 = reinterpret_cast<const floatx4*>(rows + id * dim);
+      for (int i = lane; i < dim / 4; i += 64) {
+        const floatx4 a = q4[i], b = r4[i];
+        acc = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc))));
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    }
+    if (lane == 0) {
+      sc[c] = id >= 0 ? acc : -INFINITY;
+      sid[c] = id;
+    }
+  }
+  __syncthreads();
+  if (tid < kc) {
+    int rank = 0;
+    for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
+    if (rank < k) {
+      out_s[q * k + rank] = sid[tid] >= 0 ? sc[tid] : -INFINITY;
+      out_i[q * k + rank] = sid[tid];
+    }
+  } else if (tid < k) {
+    out_s[q * k + tid] = -INFINITY;  // k > kc: padding past the candidates
+    out_i[q * k + tid] = -1;
+  }
+}
+
 // ======================================================= K10: merge lists ======
 // One block per query: every thread keeps a register top-KC of its strided share of
 // the n_lists*k_in candidates, then k_out rounds of a block arg-best pop the winners.
+// Overflow check (list_kc < k_out, i.e. the scan kept only list_kc entries per list):
+// a list whose last kept entry beats the final k_out-th result may have dropped a
+// member of the true top-k, so *overflow is set and the caller re-runs the scan with
+// full-length lists.  Lists that never filled hold padding and pass.
 template <int KC, typename IdIn>
 __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs,
                                                     const IdIn* __restrict__ ci, int n_lists,
                                                     int64_t nq, int k_in, int k_out,
                                                     float* __restrict__ out_s,
-                                                    int64_t* __restrict__ out_i) {
+                                                    int64_t* __restrict__ out_i, int list_kc,
+                                                    int* __restrict__ overflow) {
   __shared__ float red_s[4];
   __shared__ long long red_i[4];
   __shared__ int red_t[4];
+  __shared__ float kth_s;
+  __shared__ long long kth_i;
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // local lists hold int ids; shard-merge ids are int64 -> use a 64-bit twin list
@@ -253,6 +319,8 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
     if (tid == 0) {
       out_s[q * k_out + r] = bi < 0 ? -INFINITY : bs;
       out_i[q * k_out + r] = bi < 0 ? -1 : bi;
+      kth_s = bi < 0 ? -INFINITY : bs;
+      kth_i = bi;
     }
     if (tid == bt && bi >= 0) {
       // pop this thread's head
@@ -265,6 +333,16 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
       li[KC - 1] = -1;
     }
     __syncthreads();
+  }
+  if (overflow && list_kc < k_out) {
+    // entries a full list dropped are worse than its last kept one: only a last entry
+    // strictly better than the k_out-th result (or any full list, when fewer than k_out
+    // results exist) can hide a member of the top-k
+    for (int64_t lst = tid; lst < n_lists; lst += 256) {
+      const int64_t off = (lst * nq + q) * k_in + (list_kc - 1);
+      const long long xi = (long long)ci[off];
+      if (xi >= 0 && better(cs[off], xi, kth_s, kth_i)) atomicOr(overflow, 1);
+    }
   }
 }
 
@@ -300,7 +378,11 @@ struct DevBuf {
   }
 };
 
-int kc_for(int k) { return k <= 8 ? 8 : (k <= 32 ? 32 : 64); }
+// register list lengths: the fused scan keeps 8 or 16 entries per lane (k > 16 runs
+// with 16 + the merge's overflow check, re-running with 64 only when it fires); the
+// merge keeps up to 64 per thread
+int kc_scan(int k) { return k <= 8 ? 8 : 16; }
+int kc_merge(int k) { return k <= 8 ? 8 : (k <= 16 ? 16 : 64); }
 
 }  // namespace
 
@@ -313,6 +395,11 @@ struct mq_index {
   float* rows = nullptr;  // [cap, dim], every stored row unit-norm
   int num_cus = 256;
   DevBuf stage, cand_s, cand_i, out_s, out_i;
+  DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
+  int64_t n16 = 0;   // rows already mirrored into rows16
+  DevBuf q16, coarse_s, coarse_i;
+  DevBuf flag;          // merge overflow flag (k > 16)
+  int64_t rescans = 0;  // searches re-run with 64-entry lists
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -323,24 +410,28 @@ namespace {
 template <class T, int KC>
 void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int nqt,
                    float* cs, int* ci, hipStream_t s) {
-  hipLaunchKernelGGL((flat_search_kernel<T, KC>), dim3(G * nqt), dim3(256), 0, s, q, nq,
-                     ix->rows, ix->n, ix->dim, G, nqt, k, cs, ci);
+  // bf16 tiles read the bf16 shadow as float-typed rows of half the width
+  const float* rows = T::BF16 ? ix->rows16.as<float>() : ix->rows;
+  const int dim = T::BF16 ? ix->dim / 2 : ix->dim;
+  hipLaunchKernelGGL((flat_search_kernel<T, KC>), dim3(G * nqt), dim3(256), 0, s, q, nq, rows,
+                     ix->n, dim, G, nqt, k, cs, ci);
 }
 
 template <int KC, typename IdIn>
 void launch_merge(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
-                  float* os, int64_t* oi, hipStream_t s) {
+                  float* os, int64_t* oi, int list_kc, int* overflow, hipStream_t s) {
   hipLaunchKernelGGL((merge_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
-                     n_lists, nq, k_in, k_out, os, oi);
+                     n_lists, nq, k_in, k_out, os, oi, list_kc, overflow);
 }
 
 template <typename IdIn>
 void merge_dispatch(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
-                    float* os, int64_t* oi, hipStream_t s) {
-  switch (kc_for(k_out)) {
-    case 8: launch_merge<8>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
-    case 32: launch_merge<32>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
-    default: launch_merge<64>(cs, ci, n_lists, nq, k_in, k_out, os, oi, s); break;
+                    float* os, int64_t* oi, hipStream_t s, int list_kc = 1 << 30,
+                    int* overflow = nullptr) {
+  switch (kc_merge(k_out)) {
+    case 8: launch_merge<8>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
+    case 16: launch_merge<16>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
+    default: launch_merge<64>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
   }
 }
 
@@ -351,7 +442,7 @@ struct SearchPlan {
   int64_t n_lists;
 };
 
-SearchPlan plan_search(const mq_index* ix, int64_t nq, int k) {
+SearchPlan plan_search(const mq_index* ix, int64_t nq, int kc) {
   SearchPlan p;
   p.wide = nq > 64;
   const int BM = p.wide ? SearchWide::BM : SearchNarrow::BM;
@@ -360,9 +451,9 @@ SearchPlan plan_search(const mq_index* ix, int64_t nq, int k) {
   const int lpq = p.wide ? SearchSmem<SearchWide>::LPQ : SearchSmem<SearchNarrow>::LPQ;
   p.nqt = (int)((nq + BM - 1) / BM);
   const int64_t ntiles = (ix->n + BN - 1) / BN;
-  // resident 256-thread blocks per CU: 2 with the 8-entry register top list, else 1
-  // (VGPR budget); G row groups per query tile, a multiple of 8 (XCD mapping)
-  const int per_cu = kc_for(k) <= 8 ? 2 : 1;
+  // resident 256-thread blocks per CU: 2 with an 8/16-entry register top list, 1 with
+  // 64 (VGPR budget); G row groups per query tile, a multiple of 8 (XCD mapping)
+  const int per_cu = kc <= 16 ? 2 : 1;
   int64_t G = std::max<int64_t>(1, per_cu * ix->num_cus / p.nqt);
   G = std::min<int64_t>(G, ntiles);
   p.G = (int)((G + 7) / 8 * 8);
@@ -379,41 +470,112 @@ int fill_padding(float* os, int64_t* oi, int64_t count, hipStream_t s) {
   return MQ_OK;
 }
 
-// Search with queries and outputs already in device memory (asynchronous).
+enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16 };
+
+template <int KC>
+void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq, int kl, int G,
+                 int nqt, float* cs, int* ci, hipStream_t s) {
+  if (kind == SCAN_BF16) {
+    if (wide)
+      launch_search<SearchWideBF, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+    else
+      launch_search<SearchNarrowBF, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+    return;
+  }
+  if constexpr (KC <= 16) {  // (a 64-entry list spills next to the x6 operands)
+    if (kind == SCAN_X6 && wide) {
+      launch_search<SearchWideX6, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+      return;
+    }
+  }
+  if (wide)
+    launch_search<SearchWide, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+  else
+    launch_search<SearchNarrow, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+}
+
+// K9 fused scan + K10 merge -> exact top-k of the whole index for every query.
+// k <= 16 runs with lists of 8/16.  For 16 < k <= 64 the scan still keeps 16 per list
+// and the merge checks that no list overflowed (see merge_kernel); if one did, the
+// batch is re-scanned with 64-entry lists, so results are exact either way.  The
+// check costs one 4-byte device->host read, i.e. k > 16 calls are synchronous.
+int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+              hipStream_t s) {
+  int kc = kc_scan(k);
+  for (;;) {
+    const int kl = std::min(kc, k);
+    const bool check = kl < k;
+    const SearchPlan p = plan_search(ix, nq, kc);
+    const size_t n_cand = (size_t)p.n_lists * nq * kl;
+    int rc = ix->cand_s.ensure(n_cand * sizeof(float));
+    if (!rc) rc = ix->cand_i.ensure(n_cand * sizeof(int));
+    if (!rc && check) rc = ix->flag.ensure(sizeof(int));
+    if (rc) return rc;
+    float* cs = ix->cand_s.as<float>();
+    int* ci = ix->cand_i.as<int>();
+    int* flag = check ? ix->flag.as<int>() : nullptr;
+    if (flag) MQ_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    if (ix->tl.used > 4096) ix->tl.drain();
+    ix->tl.mark(s, 0);
+    switch (kc) {
+      case 8: launch_scan<8>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      case 16: launch_scan<16>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+    }
+    MQ_HIP(hipGetLastError());
+    ix->tl.mark(s, 1);
+    merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, kl, k, os, oi, s, kl, flag);
+    ix->tl.close(s);
+    MQ_HIP(hipGetLastError());
+    if (!flag) return MQ_OK;
+    int overflow = 0;
+    MQ_HIP(hipMemcpyAsync(&overflow, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    MQ_HIP(hipStreamSynchronize(s));
+    if (!overflow) return MQ_OK;
+    ++ix->rescans;
+    kc = MQ_MAX_K;
+    if (kind == SCAN_X6) kind = SCAN_F32;
+  }
+}
+
+// Config 5: bf16 coarse scan for the best `kc` rows per query (kc = max(2k, 50) capped
+// at MQ_MAX_K and n), then an exact fp32 re-rank of those candidates to the final top-k.
+int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+                       hipStream_t s) {
+  const int64_t dim = ix->dim;
+  int rc = ix->rows16.ensure((size_t)ix->cap * dim * 2);
+  if (rc) return rc;
+  if (ix->n16 < ix->n) {  // mirror rows added since the last bf16 search
+    const int64_t pairs = (ix->n - ix->n16) * dim / 2;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s,
+                       ix->rows + ix->n16 * dim, ix->rows16.as<unsigned>() + ix->n16 * dim / 2,
+                       pairs);
+    ix->n16 = ix->n;
+  }
+  rc = ix->q16.ensure((size_t)nq * dim * 2);
+  if (rc) return rc;
+  const int64_t qpairs = nq * dim / 2;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((qpairs + 255) / 256)), dim3(256), 0, s, q,
+                     ix->q16.as<unsigned>(), qpairs);
+  const int kc = (int)std::min<int64_t>(std::max(2 * k, 50), std::min<int64_t>(MQ_MAX_K, ix->n));
+  rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
+  if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
+  if (!rc) rc = scan_topk(ix, SCAN_BF16, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(),
+                          ix->coarse_i.as<int64_t>(), s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+                     ix->coarse_i.as<int64_t>(), kc, k, os, oi);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+// Search with queries and outputs already in device memory (asynchronous for k <= 16).
 int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                   hipStream_t s) {
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
-  const SearchPlan p = plan_search(ix, nq, k);
-  const size_t n_cand = (size_t)p.n_lists * nq * k;
-  int rc = ix->cand_s.ensure(n_cand * sizeof(float));
-  if (rc) return rc;
-  rc = ix->cand_i.ensure(n_cand * sizeof(int));
-  if (rc) return rc;
-  float* cs = ix->cand_s.as<float>();
-  int* ci = ix->cand_i.as<int>();
-  const int kc = kc_for(k);
-#define MQ_SEARCH(T)                                                           \
-  switch (kc) {                                                                \
-    case 8: launch_search<T, 8>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break;   \
-    case 32: launch_search<T, 32>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
-    default: launch_search<T, 64>(ix, q, (int)nq, k, p.G, p.nqt, cs, ci, s); break; \
-  }
-  if (ix->tl.used > 4096) ix->tl.drain();
-  ix->tl.mark(s, 0);
-  if (p.wide && ix->precision == MQ_DTYPE_F32X6) {
-    MQ_SEARCH(SearchWideX6)
-  } else if (p.wide) {
-    MQ_SEARCH(SearchWide)
-  } else {
-    MQ_SEARCH(SearchNarrow)
-  }
-#undef MQ_SEARCH
-  MQ_HIP(hipGetLastError());
-  ix->tl.mark(s, 1);
-  merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, k, k, os, oi, s);
-  ix->tl.close(s);
-  MQ_HIP(hipGetLastError());
-  return MQ_OK;
+  if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
+    return search_bf16_rerank(ix, q, nq, k, os, oi, s);
+  return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
 }
 
 int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
@@ -431,6 +593,7 @@ int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
   if (ix->rows) MQ_HIP(hipFree(ix->rows));
   ix->rows = fresh;
   ix->cap = new_cap;
+  ix->n16 = 0;  // the bf16 shadow is rebuilt at the next coarse search
   return MQ_OK;
 }
 
@@ -484,6 +647,11 @@ int mq_index_destroy(mq_index* ix) {
     ix->cand_i.release();
     ix->out_s.release();
     ix->out_i.release();
+    ix->rows16.release();
+    ix->q16.release();
+    ix->coarse_s.release();
+    ix->coarse_i.release();
+    ix->flag.release();
   }
   delete ix;
   return MQ_OK;
@@ -515,6 +683,7 @@ int mq_index_reset(mq_index* ix) {
   MQ_CHECK_ARG(ix, "NULL index");
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->n = 0;
+  ix->n16 = 0;
   return MQ_OK;
 }
 
@@ -596,8 +765,10 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
 int mq_index_set_precision(mq_index* ix, int dtype) {
   clear_error();
   MQ_CHECK_ARG(ix, "NULL index");
-  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6,
-               "search precision must be MQ_DTYPE_F32 or MQ_DTYPE_F32X6 (got %d)", dtype);
+  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6 || dtype == MQ_DTYPE_BF16,
+               "search precision must be MQ_DTYPE_F32, MQ_DTYPE_F32X6 or MQ_DTYPE_BF16 (got %d)",
+               dtype);
+  MQ_CHECK_ARG(dtype != MQ_DTYPE_BF16 || ix->dim % 64 == 0, "bf16 coarse scan needs dim %% 64 == 0");
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->precision = dtype;
   return MQ_OK;
@@ -670,6 +841,7 @@ int mq_index_load(mq_index* ix, const char* path) {
             ix->dim, ix->dtype);
   }
   ix->n = 0;
+  ix->n16 = 0;
   int rc = reserve_rows(ix, h.n_rows, nullptr);
   if (rc) {
     fclose(f);
