@@ -79,7 +79,10 @@ int mq_index_add(mq_index* ix, const float* rows, int64_t n, int rows_on_device,
 int mq_index_reset(mq_index* ix);
 /* Exact top-k (K9 fused score + per-block top-k, K10 merge).
  * queries [nq, dim] f32; out_scores [nq, k] f32; out_ids [nq, k] int64.
- * All three host (io_on_device = 0) or all device (io_on_device = 1). 1 <= k <= MQ_MAX_K. */
+ * All three host (io_on_device = 0) or all device (io_on_device = 1). 1 <= k <= MQ_MAX_K.
+ * Device calls are asynchronous on `stream` for k <= 16; for k > 16 the call reads a
+ * 4-byte overflow flag back (the scan keeps 16 candidates per list and re-scans with
+ * 64 when a list may have dropped a top-k member), so it returns after the search. */
 int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
                     float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
 /* Copy stored (normalised) rows [row0, row0 + n) into out [n, dim] f32 (host or device). */
@@ -90,6 +93,12 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
  * at MQ_MAX_K) candidates, then an exact fp32 re-rank to the top-k (BASELINE config 5;
  * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0. */
 int mq_index_set_precision(mq_index* ix, int dtype);
+/* Batches of at most `max_queries` queries (default 4, 0..16; dim % 64 == 0, dim <= 1024)
+ * use the streaming fp32 kernel instead of the MFMA tiles, whatever the precision. */
+int mq_index_set_stream_threshold(mq_index* ix, int max_queries);
+/* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
+ * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
+int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
 /* Device-time accounting with HIP events on the launch stream (off by default).
@@ -107,7 +116,9 @@ int mq_index_load(mq_index* ix, const char* path);
  * padding.  Pure CPU, no device needed. */
 int mq_topk_merge_host(const float* scores, const int64_t* ids, int n_lists, int64_t nq,
                        int k_in, int k_out, float* out_scores, int64_t* out_ids);
-/* Same merge on the device (inputs/outputs device pointers, async on stream). */
+/* Same merge on the device (inputs/outputs device pointers, async on stream).  Each
+ * input list must be sorted (score desc, id asc, padding last), as mq_index_search
+ * returns it: the kernel stops reading a list at its first non-qualifying entry. */
 int mq_topk_merge_device(const float* scores, const int64_t* ids, int n_lists, int64_t nq,
                          int k_in, int k_out, float* out_scores, int64_t* out_ids, void* stream);
 

@@ -183,6 +183,89 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
   }
 }
 
+// ============================================ K9s: streaming scan, few queries ==
+// For a handful of queries the MFMA tiles above are mostly padding (32 query rows per
+// tile) while the row stream is what bounds the scan, so small batches use a plain
+// streaming dot-product kernel instead: 16 lanes per row (each 16-B load instruction
+// of a wave covers four 256-B row segments), queries in LDS, two rows in flight per
+// lane group, fp32 FMA, a 16-lane butterfly per (row, query), and lane j of the group
+// keeps query j's register top list.  List = lane group: cand[group][query][0..kl).
+constexpr int kStreamMaxNV = 16;  // float4 per lane per row: dim <= 1024
+
+template <int NQ, int KC, int NV>
+__global__ __launch_bounds__(256) void stream_search_kernel(const float* __restrict__ Q, int nq,
+                                                            const float* __restrict__ C,
+                                                            int64_t n_rows, int dim, int kl,
+                                                            float* __restrict__ cand_s,
+                                                            int* __restrict__ cand_i) {
+  extern __shared__ __attribute__((aligned(16))) float qs[];  // [NQ][dim], zero padded
+  const int tid = threadIdx.x, gl = tid & 15;
+  for (int i = tid; i < NQ * dim; i += 256) {
+    const int j = i / dim;
+    qs[i] = j < nq ? Q[(int64_t)j * dim + (i - j * dim)] : 0.f;
+  }
+  __syncthreads();
+  const int nv = NV == kStreamMaxNV ? dim >> 6 : NV;  // NV < max: compiled for dim = 64 NV
+  const int64_t group = (int64_t)blockIdx.x * 16 + (tid >> 4);
+  const int64_t n_groups = (int64_t)gridDim.x * 16;
+  TopList<KC> top;
+  top.init();
+  const bool owner = gl < nq && gl < NQ;  // lane gl keeps query gl's list
+  const float* qbase = qs + gl * 4;
+
+  auto score_rows = [&](const floatx4 (&v)[2][NV], int64_t r0, int nr)
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mine = 0.f;
+      // one query at a time: 12 ds_read_b128 of its slice, 48 FMA, 16-lane butterfly
+      constexpr int kUnrollQ = NQ <= 2 ? NQ : 1;
+#pragma unroll kUnrollQ
+      for (int j = 0; j < NQ; ++j) {
+        const float* qj = qbase + j * dim;
+        if constexpr (NQ > 2) asm volatile("" : "+v"(qj));
+        float acc = 0.f;
+#pragma unroll
+        for (int it = 0; it < NV; ++it) {
+          if (it < nv) {
+            const floatx4 qv = *reinterpret_cast<const floatx4*>(qj + it * 64);
+            acc = fmaf(v[u][it].x, qv.x, fmaf(v[u][it].y, qv.y,
+                  fmaf(v[u][it].z, qv.z, fmaf(v[u][it].w, qv.w, acc))));
+          }
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+        mine = gl == j ? acc : mine;
+      }
+      const int64_t r = r0 + u * n_groups;
+      if (u < nr && owner && top.beats_tail(mine, (int)r)) top.insert(mine, (int)r);
+    }
+  };
+
+  for (int64_t r0 = group; r0 < n_rows; r0 += 2 * n_groups) {
+    const int nr = r0 + n_groups < n_rows ? 2 : 1;
+    floatx4 v[2][NV];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const floatx4* rp =
+          reinterpret_cast<const floatx4*>(C + (u < nr ? r0 + u * n_groups : r0) * dim) + gl;
+#pragma unroll
+      for (int it = 0; it < NV; ++it)
+        if (it < nv) v[u][it] = __builtin_nontemporal_load(rp + it * 16);
+    }
+    score_rows(v, r0, nr);
+  }
+  if (owner) {
+    const int64_t base = (group * nq + gl) * kl;
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+      if (i < kl) {
+        cand_s[base + i] = top.s[i];
+        cand_i[base + i] = top.id[i];
+      }
+  }
+}
+
 // ================================================= bf16 coarse path (config 5) ==
 // fp32 -> bf16 (round to nearest even), two elements per thread.
 __global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ src,
@@ -238,12 +321,17 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
 }
 
 // ======================================================= K10: merge lists ======
-// One block per query: every thread keeps a register top-KC of its strided share of
-// the n_lists*k_in candidates, then k_out rounds of a block arg-best pop the winners.
-// Overflow check (list_kc < k_out, i.e. the scan kept only list_kc entries per list):
-// a list whose last kept entry beats the final k_out-th result may have dropped a
-// member of the true top-k, so *overflow is set and the caller re-runs the scan with
-// full-length lists.  Lists that never filled hold padding and pass.
+// One block per query.  Each list is sorted, so a thread walks its share of the lists
+// (lists tid, tid+256, ...) reading heads in batches of 8 independent loads, and only
+// a head that beats its register top-KC tail pulls further entries of that list.
+// Then every wave pops its 64 lanes' best k_out (shuffle arg-best, no block barrier),
+// and the 4*k_out wave winners are ranked against each other in LDS to place them.
+// Overflow checks (results stay exact; the caller re-runs on a set bit):
+//  bit 0 (list_kc < k_out, the scan kept only list_kc entries per list): a list whose
+//        last kept entry beats the final k_out-th result may have dropped a member of
+//        the top-k -> re-scan with full-length lists.  Unfilled lists hold padding.
+//  bit 1 (KC < k_out, 16-entry thread lists for large k): same test on each thread's
+//        register list -> re-run only this merge with KC = 64.
 template <int KC, typename IdIn>
 __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs,
                                                     const IdIn* __restrict__ ci, int n_lists,
@@ -251,9 +339,9 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
                                                     float* __restrict__ out_s,
                                                     int64_t* __restrict__ out_i, int list_kc,
                                                     int* __restrict__ overflow) {
-  __shared__ float red_s[4];
-  __shared__ long long red_i[4];
-  __shared__ int red_t[4];
+  constexpr int U = 8;
+  __shared__ float ws[4 * MQ_MAX_K];
+  __shared__ long long wi[4 * MQ_MAX_K];
   __shared__ float kth_s;
   __shared__ long long kth_i;
   const int64_t q = blockIdx.x;
@@ -266,14 +354,7 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
     ls[i] = -INFINITY;
     li[i] = -1;
   }
-  const int64_t n_items = (int64_t)n_lists * k_in;
-  for (int64_t it = tid; it < n_items; it += 256) {
-    const int64_t lst = it / k_in, kk = it % k_in;
-    const int64_t off = (lst * nq + q) * k_in + kk;
-    float x = cs[off];
-    long long xi = (long long)ci[off];
-    if (xi < 0) continue;
-    if (!better(x, xi, ls[KC - 1], li[KC - 1])) continue;
+  auto push = [&](float x, long long xi) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       const bool sw = better(x, xi, ls[i], li[i]);
@@ -284,11 +365,42 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
       x = sw ? ts : x;
       xi = sw ? ti : xi;
     }
+  };
+  for (int l0 = tid; l0 < n_lists; l0 += 256 * U) {
+    float hs[U];
+    long long hi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int lst = l0 + 256 * u;
+      hs[u] = -INFINITY;
+      hi[u] = -1;
+      if (lst < n_lists) {
+        const int64_t off = ((int64_t)lst * nq + q) * k_in;
+        hs[u] = cs[off];
+        hi[u] = (long long)ci[off];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (hi[u] < 0 || !better(hs[u], hi[u], ls[KC - 1], li[KC - 1])) continue;
+      push(hs[u], hi[u]);
+      const int64_t off = ((int64_t)(l0 + 256 * u) * nq + q) * k_in;
+      for (int kk = 1; kk < k_in; ++kk) {  // rest of a sorted list, while it still beats
+        const float x = cs[off + kk];
+        const long long xi = (long long)ci[off + kk];
+        if (xi < 0 || !better(x, xi, ls[KC - 1], li[KC - 1])) break;
+        push(x, xi);
+      }
+    }
   }
+  // thread-list overflow (KC < k_out): remember this thread's KC-th entry
+  const float tail_s = ls[KC - 1];
+  const long long tail_i = li[KC - 1];
+  // per-wave arg-best rounds: wave winners in order into ws/wi[wave * k_out + r]
   for (int r = 0; r < k_out; ++r) {
     float bs = ls[0];
     long long bi = li[0];
-    int bt = tid;
+    int bt = lane;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const float os = __shfl_xor(bs, off);
@@ -301,29 +413,10 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
       }
     }
     if (lane == 0) {
-      red_s[wave] = bs;
-      red_i[wave] = bi;
-      red_t[wave] = bt;
+      ws[wave * k_out + r] = bs;
+      wi[wave * k_out + r] = bi;
     }
-    __syncthreads();
-    bs = red_s[0];
-    bi = red_i[0];
-    bt = red_t[0];
-#pragma unroll
-    for (int w = 1; w < 4; ++w)
-      if (better(red_s[w], red_i[w], bs, bi)) {
-        bs = red_s[w];
-        bi = red_i[w];
-        bt = red_t[w];
-      }
-    if (tid == 0) {
-      out_s[q * k_out + r] = bi < 0 ? -INFINITY : bs;
-      out_i[q * k_out + r] = bi < 0 ? -1 : bi;
-      kth_s = bi < 0 ? -INFINITY : bs;
-      kth_i = bi;
-    }
-    if (tid == bt && bi >= 0) {
-      // pop this thread's head
+    if (lane == bt && bi >= 0) {  // pop this lane's head
 #pragma unroll
       for (int i = 0; i + 1 < KC; ++i) {
         ls[i] = ls[i + 1];
@@ -332,14 +425,49 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
       ls[KC - 1] = -INFINITY;
       li[KC - 1] = -1;
     }
+  }
+  if (tid == 0) {
+    kth_s = -INFINITY;
+    kth_i = -1;
+  }
+  __syncthreads();
+  // rank the 4*k_out wave winners; valid ids are distinct, so valid ranks are too
+  const int nc = 4 * k_out;
+  for (int c = tid; c < nc; c += 256) {
+    const float x = ws[c];
+    const long long xi = wi[c];
+    if (xi < 0) continue;
+    int rank = 0;
+    for (int u = 0; u < nc; ++u) rank += (wi[u] >= 0 && better(ws[u], wi[u], x, xi)) ? 1 : 0;
+    if (rank < k_out) {
+      out_s[q * k_out + rank] = x;
+      out_i[q * k_out + rank] = xi;
+      if (rank == k_out - 1) {
+        kth_s = x;
+        kth_i = xi;
+      }
+    }
+  }
+  // padding past the valid results
+  int nvalid = 0;
+  for (int u = 0; u < nc; ++u) nvalid += wi[u] >= 0 ? 1 : 0;
+  for (int r = nvalid + tid; r < k_out; r += 256) {
+    out_s[q * k_out + r] = -INFINITY;
+    out_i[q * k_out + r] = -1;
+  }
+  if (KC < k_out) {
+    // a thread holding KC entries that all beat the k_out-th result may have dropped
+    // more: bit 1 asks the caller to re-run the merge with 64-entry thread lists
     __syncthreads();
+    if (overflow && tail_i >= 0 && better(tail_s, tail_i, kth_s, kth_i)) atomicOr(overflow, 2);
   }
   if (overflow && list_kc < k_out) {
+    __syncthreads();
     // entries a full list dropped are worse than its last kept one: only a last entry
     // strictly better than the k_out-th result (or any full list, when fewer than k_out
     // results exist) can hide a member of the top-k
-    for (int64_t lst = tid; lst < n_lists; lst += 256) {
-      const int64_t off = (lst * nq + q) * k_in + (list_kc - 1);
+    for (int lst = tid; lst < n_lists; lst += 256) {
+      const int64_t off = ((int64_t)lst * nq + q) * k_in + (list_kc - 1);
       const long long xi = (long long)ci[off];
       if (xi >= 0 && better(cs[off], xi, kth_s, kth_i)) atomicOr(overflow, 1);
     }
@@ -347,7 +475,6 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
 }
 
 }  // namespace mq
-
 
 // ================================================================ host side =====
 using namespace mq;
@@ -399,7 +526,9 @@ struct mq_index {
   int64_t n16 = 0;   // rows already mirrored into rows16
   DevBuf q16, coarse_s, coarse_i;
   DevBuf flag;          // merge overflow flag (k > 16)
-  int64_t rescans = 0;  // searches re-run with 64-entry lists
+  int64_t rescans = 0;   // searches re-run with 64-entry scan lists
+  int64_t remerges = 0;  // merges re-run with 64-entry thread lists
+  int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -427,8 +556,8 @@ void launch_merge(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int 
 template <typename IdIn>
 void merge_dispatch(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
                     float* os, int64_t* oi, hipStream_t s, int list_kc = 1 << 30,
-                    int* overflow = nullptr) {
-  switch (kc_merge(k_out)) {
+                    int* overflow = nullptr, int kc = 0) {
+  switch (kc ? kc : kc_merge(k_out)) {
     case 8: launch_merge<8>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
     case 16: launch_merge<16>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
     default: launch_merge<64>(cs, ci, n_lists, nq, k_in, k_out, os, oi, list_kc, overflow, s); break;
@@ -470,7 +599,39 @@ int fill_padding(float* os, int64_t* oi, int64_t count, hipStream_t s) {
   return MQ_OK;
 }
 
-enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16 };
+enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16, SCAN_STREAM };
+
+template <int NQ, int KC>
+void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
+                      int* ci, hipStream_t s) {
+  const size_t lds = (size_t)NQ * ix->dim * sizeof(float);
+  if (ix->dim == 768)  // the dmeta / BERT-base width, register arrays sized exactly
+    hipLaunchKernelGGL((stream_search_kernel<NQ, KC, 12>), dim3(blocks), dim3(256), lds, s, q, nq,
+                       ix->rows, ix->n, ix->dim, kl, cs, ci);
+  else
+    hipLaunchKernelGGL((stream_search_kernel<NQ, KC, kStreamMaxNV>), dim3(blocks), dim3(256), lds,
+                       s, q, nq, ix->rows, ix->n, ix->dim, kl, cs, ci);
+}
+
+template <int KC>
+void launch_stream(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
+                   int* ci, hipStream_t s) {
+  if (nq <= 1)
+    launch_stream_nq<1, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+  else if (nq <= 2)
+    launch_stream_nq<2, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+  else if (nq <= 4)
+    launch_stream_nq<4, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+  else if (nq <= 8)
+    launch_stream_nq<8, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+  else
+    launch_stream_nq<16, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+}
+
+// streaming-kernel grid: up to 2 blocks per CU, at least ~8 rows per lane group
+int stream_blocks(const mq_index* ix) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(2 * ix->num_cus, (ix->n + 127) / 128));
+}
 
 template <int KC>
 void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq, int kl, int G,
@@ -505,7 +666,8 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
   for (;;) {
     const int kl = std::min(kc, k);
     const bool check = kl < k;
-    const SearchPlan p = plan_search(ix, nq, kc);
+    SearchPlan p = plan_search(ix, nq, kc);
+    if (kind == SCAN_STREAM) p.n_lists = (int64_t)stream_blocks(ix) * 16;
     const size_t n_cand = (size_t)p.n_lists * nq * kl;
     int rc = ix->cand_s.ensure(n_cand * sizeof(float));
     if (!rc) rc = ix->cand_i.ensure(n_cand * sizeof(int));
@@ -517,24 +679,41 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
     if (flag) MQ_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
     if (ix->tl.used > 4096) ix->tl.drain();
     ix->tl.mark(s, 0);
-    switch (kc) {
+    if (kind == SCAN_STREAM) {
+      const int nb = stream_blocks(ix);
+      switch (kc) {
+        case 8: launch_stream<8>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+        case 16: launch_stream<16>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+        default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+      }
+    } else switch (kc) {
       case 8: launch_scan<8>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
       case 16: launch_scan<16>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
       default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
     }
     MQ_HIP(hipGetLastError());
     ix->tl.mark(s, 1);
-    merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, kl, k, os, oi, s, kl, flag);
+    // k > 16: 16-entry thread lists in the merge too (KC = 64 costs ~20x more)
+    const int merge_kc = flag ? 16 : kc_merge(k);
+    merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, kl, k, os, oi, s, kl, flag, merge_kc);
     ix->tl.close(s);
     MQ_HIP(hipGetLastError());
     if (!flag) return MQ_OK;
     int overflow = 0;
     MQ_HIP(hipMemcpyAsync(&overflow, flag, sizeof(int), hipMemcpyDeviceToHost, s));
     MQ_HIP(hipStreamSynchronize(s));
-    if (!overflow) return MQ_OK;
-    ++ix->rescans;
-    kc = MQ_MAX_K;
-    if (kind == SCAN_X6) kind = SCAN_F32;
+    if (overflow & 1) {  // a scan list overflowed: re-scan with full-length lists
+      ++ix->rescans;
+      kc = MQ_MAX_K;
+      if (kind == SCAN_X6) kind = SCAN_F32;
+      continue;
+    }
+    if (overflow & 2) {  // only a merge thread list overflowed: re-merge with KC = 64
+      ++ix->remerges;
+      merge_dispatch<int>(cs, ci, (int)p.n_lists, nq, kl, k, os, oi, s, kl, nullptr, MQ_MAX_K);
+      MQ_HIP(hipGetLastError());
+    }
+    return MQ_OK;
   }
 }
 
@@ -573,6 +752,9 @@ int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* o
 int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                   hipStream_t s) {
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
+  // few queries: exact fp32 streaming scan, whatever the precision setting
+  if (nq <= ix->stream_max_q && ix->dim % 64 == 0 && ix->dim <= 64 * kStreamMaxNV)
+    return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
   return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
@@ -771,6 +953,24 @@ int mq_index_set_precision(mq_index* ix, int dtype) {
   MQ_CHECK_ARG(dtype != MQ_DTYPE_BF16 || ix->dim % 64 == 0, "bf16 coarse scan needs dim %% 64 == 0");
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->precision = dtype;
+  return MQ_OK;
+}
+
+int mq_index_set_stream_threshold(mq_index* ix, int max_queries) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(max_queries >= 0 && max_queries <= 16, "stream threshold must be in [0, 16] (got %d)",
+               max_queries);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->stream_max_q = max_queries;
+  return MQ_OK;
+}
+
+int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL argument");
+  if (rescans) *rescans = ix->rescans;
+  if (remerges) *remerges = ix->remerges;
   return MQ_OK;
 }
 

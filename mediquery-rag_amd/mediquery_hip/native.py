@@ -75,8 +75,27 @@ class FlatIndex:
     STAGES = ("flat_search_kernel", "merge_kernel")
 
     def set_precision(self, dtype):
-        """_lib.MQ_DTYPE_F32 (exact f32 MFMA) or _lib.MQ_DTYPE_F32X6 (split-f32)."""
+        """_lib.MQ_DTYPE_F32 (exact f32 MFMA), _lib.MQ_DTYPE_F32X6 (split-f32) or
+        _lib.MQ_DTYPE_BF16 (bf16 coarse scan + exact fp32 re-rank)."""
         _lib.call("mq_index_set_precision", self._h, dtype)
+
+    def set_stream_threshold(self, max_queries):
+        """Batches of <= max_queries (0..16) use the streaming fp32 kernel (K9s)."""
+        _lib.call("mq_index_set_stream_threshold", self._h, int(max_queries))
+
+    @property
+    def rescans(self):
+        """Searches whose k > 16 list-overflow check fired (re-scanned with 64 lists)."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_rescans", self._h, ctypes.byref(n), None)
+        return n.value
+
+    @property
+    def remerges(self):
+        """Merges whose 16-entry thread lists overflowed (re-run with 64)."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_rescans", self._h, None, ctypes.byref(n))
+        return n.value
 
     def set_timing(self, enabled=True):
         _lib.call("mq_index_set_timing", self._h, int(bool(enabled)))

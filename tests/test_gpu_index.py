@@ -53,6 +53,69 @@ def test_shapes_vs_oracle(require_gpu, n, nq, k, prec):
         assert (i[:, n:] == -1).all() and np.isneginf(s[:, n:]).all()
 
 
+@pytest.mark.parametrize("dim", [768, 128, 1024])
+@pytest.mark.parametrize("n", [777, 20000])
+def test_small_batch_stream_and_mfma_paths(require_gpu, dim, n):
+    """Small batches (nq <= threshold) run the streaming fp32 kernel (K9s); threshold 0
+    sends the same batches to the narrow MFMA tiles.  Both must match the oracle, for
+    every NQ specialisation (1, 2, 4, 8, 16) and list length (8, 16, 16+rescan)."""
+    c = synth.corpus(n, dim, seed=dim + n, clustered=True)
+    ref_q, _ = synth.queries(16, c, seed=5)
+    ref = exact_scores(ref_q, c)
+    ix = _index(c)
+    for thr in (16, 0):
+        ix.set_stream_threshold(thr)
+        for nq in (1, 2, 3, 5, 8, 13, 16):
+            for k in (1, 5, 17, 50):
+                s, i = ix.search(ref_q[:nq], k)
+                assert check_topk(i, s, ref[:nq], k) == [], (thr, nq, k)
+
+
+def test_stream_kernel_overflow_rescan(require_gpu):
+    """Streaming kernel (K9s) list overflow: lane group g scans rows g, g+G, g+2G, ...
+    (G = 16 x blocks, blocks = min(2 x CUs, ceil(n/128))); 20 copies of one row placed
+    G apart all land in one group, so k = 20 must fire the check and re-scan."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 24 * 16 * 2 * cus
+    G = 16 * min(2 * cus, (n + 127) // 128)
+    rng = np.random.default_rng(5)
+    c = rng.standard_normal((n, 768), dtype=np.float32)
+    ids = 7 + G * np.arange(20)
+    c[ids] = c[7]
+    ix = _index(c)
+    q = c[7:8] / np.linalg.norm(c[7])
+    before = ix.rescans
+    s, i = ix.search(q, 20)
+    assert ix.rescans == before + 1
+    assert i[0].tolist() == ids.tolist()
+
+
+def test_merge_thread_list_overflow_remerge(require_gpu):
+    """k > 16 also merges with 16-entry thread lists (merge thread t reads scan lists
+    t, t+256, ...).  At B = 100 (wide tiles, 2 lists per 128-row tile: list = 2*tile +
+    half for the first G tiles) 15 copies in tile 3 (list 6) and 9 in tile 131 (list
+    262) put 24 top-k members in merge thread 6, while no scan list is full of copies:
+    the merge must re-run with 64-entry lists and stay exact."""
+    nq, n = 100, 128 * 1024
+    rng = np.random.default_rng(9)
+    c = rng.standard_normal((n, 768), dtype=np.float32)
+    blk_a = np.arange(15) + 128 * 3
+    blk_b = np.arange(9) + 128 * 131
+    c[blk_a] = c[blk_a[0]]
+    c[blk_b] = c[blk_a[0]]
+    q = np.repeat(c[blk_a[0]:blk_a[0] + 1], nq, axis=0) / np.linalg.norm(c[blk_a[0]])
+    ix = _index(c)
+    r0, m0 = ix.rescans, ix.remerges
+    s, i = ix.search(q, 30)
+    assert (i[:, :24] == np.concatenate([blk_a, blk_b])).all()
+    assert ix.rescans == r0
+    assert ix.remerges == m0 + 1
+    ref = exact_scores(q[:2], c)
+    assert check_topk(i[:2], s[:2], ref, 30) == []
+    np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
+
+
 def test_other_dims(require_gpu):
     for dim in (32, 256, 1024):
         c = synth.corpus(900, dim, seed=dim)
@@ -64,11 +127,17 @@ def test_other_dims(require_gpu):
 def test_duplicates_and_exact_ties(require_gpu):
     c = synth.corpus(300, 768)
     c[200] = c[10]          # exact duplicate rows: ids must come out in row order
-    c[201] = 3.0 * c[10]    # same direction, different norm -> same cosine after K8
+    c[201] = 3.0 * c[10]    # same direction, different norm -> same cosine up to rounding
     q = c[10:11] / np.linalg.norm(c[10])
-    s, i = _index(c).search(q, 3)
-    assert i[0].tolist() == [10, 200, 201]
-    np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
+    ix = _index(c)
+    for thr in (16, 0):     # streaming kernel and MFMA tiles
+        ix.set_stream_threshold(thr)
+        s, i = ix.search(q, 3)
+        got = i[0].tolist()
+        assert sorted(got) == [10, 200, 201]
+        assert got.index(10) < got.index(200)   # bit-identical rows tie -> row order
+        assert s[0][got.index(10)] == s[0][got.index(200)]
+        np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
 
 
 def test_empty_append_reset_get(require_gpu, tmp_path):
@@ -191,7 +260,10 @@ def test_large_k_list_overflow_rescan(require_gpu, prec, nq):
     q[1:] = q[1:] + 0.001 * rng.standard_normal(q[1:].shape).astype(np.float32)
     ix = _index(c, prec)
     for k in (17, 50, 64):
+        before = ix.rescans
         s, i = ix.search(q, k)
+        if nq > 8:   # tiled scan: the block of copies is one row tile -> one list
+            assert ix.rescans == before + 1
         assert (i[0, :min(k, 60)] == np.arange(4000, 4000 + min(k, 60))).all(), (k, i[0])
         if prec != _lib.MQ_DTYPE_BF16:
             ref = exact_scores(q, c)

@@ -12,12 +12,59 @@ from mediquery_hip import _lib, synth  # noqa: E402
 from mediquery_hip.native import FlatIndex  # noqa: E402
 
 
+def small_batch_crossover(ix, rows, dev, batches=(1, 2, 4, 8, 16, 32), k=5):
+    """Streaming kernel (threshold 16) vs narrow MFMA tiles (threshold 0) per batch."""
+    out = {}
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    for B in batches:
+        q, _ = synth.queries_device(B, rows)
+        s = torch.empty((B, k), device=dev)
+        i = torch.empty((B, k), dtype=torch.int64, device=dev)
+        for thr in (16, 0):
+            ix.set_stream_threshold(thr)
+            for _ in range(3):
+                ix.search_device(q, k, s, i)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                ix.search_device(q, k, s, i)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 10
+            name = "stream" if thr else "mfma"
+            out["B%d/%s" % (B, name)] = round(ms, 4)
+            print("B=%3d %-6s %7.3f ms  (%.0f GB/s row stream)" % (B, name, ms, rows.numel() * 4 / ms / 1e6),
+                  flush=True)
+    ix.set_stream_threshold(8)
+    # stage split (scan vs merge) and overflow re-scans at k = 5 / 50
+    for B, prec in ((1, 0), (8, 0), (64, 0), (256, 0), (256, _lib.MQ_DTYPE_F32X6), (256, _lib.MQ_DTYPE_BF16),
+                    (1024, _lib.MQ_DTYPE_BF16)):
+        ix.set_precision(prec)
+        q, _ = synth.queries_device(B, rows)
+        for kk in (5, 50):
+            s = torch.empty((B, kk), device=dev)
+            i = torch.empty((B, kk), dtype=torch.int64, device=dev)
+            ix.search_device(q, kk, s, i)
+            torch.cuda.synchronize()
+            r0 = ix.rescans
+            ix.set_timing(True)
+            for _ in range(5):
+                ix.search_device(q, kk, s, i)
+            t = ix.read_timing()
+            ix.set_timing(False)
+            print("B=%4d k=%2d prec %d stages %s rescans %d" % (B, kk, prec, {a: round(b / 5, 4) for a, b in t.items()},
+                                                               ix.rescans - r0), flush=True)
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    return out
+
+
 def main(n=1_000_000, batches=(1, 256, 1024), ks=(5, 50)):
     dev = torch.device("cuda", 0)
     rows = synth.corpus_device(n, 768, dev)
     ix = FlatIndex(dim=768, capacity=n)
     ix.add_device(rows)
-    res = {}
+    res = {"crossover": small_batch_crossover(ix, rows, dev)}
     for B in batches:
         q, planted = synth.queries_device(B, rows)
         for k in ks:
