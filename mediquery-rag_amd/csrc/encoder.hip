@@ -623,6 +623,18 @@ struct mq_encoder {
   size_t io_tokens = 0;
   Timeline tl;
   int num_cus = 256;
+  // Replayed forwards: one hipGraph per (B, L, precision, buffer set), captured on a
+  // private stream from io_ids/io_mask to io_out and launched on the caller's stream.
+  struct Graph {
+    int B = 0, L = 0, precision = 0;
+    std::vector<const void*> bufs;
+    hipGraphExec_t exec = nullptr;
+    uint64_t last_use = 0;
+  };
+  std::vector<Graph> graphs;
+  bool use_graphs = true;
+  uint64_t graph_clock = 0;
+  hipStream_t cap_stream = nullptr;
   std::mutex mu;
 };
 
@@ -689,6 +701,73 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
 
 }  // namespace
 
+namespace {
+
+int forward(mq_encoder* e, const int* ids, const int* mask, int B, int L, float* out,
+            hipStream_t s) {
+  switch (e->cfg.hidden) {
+    case 256: return forward_vpl<1>(e, ids, mask, B, L, out, s);
+    case 512: return forward_vpl<2>(e, ids, mask, B, L, out, s);
+    case 768: return forward_vpl<3>(e, ids, mask, B, L, out, s);
+    default: return forward_vpl<4>(e, ids, mask, B, L, out, s);
+  }
+}
+
+constexpr size_t kMaxGraphs = 6;
+
+// Replay the forward io_ids/io_mask -> io_out for (B, L) as one hipGraph launch on s,
+// capturing it first if no cached graph matches the shape, precision and buffers.
+int launch_graph(mq_encoder* e, int B, int L, hipStream_t s) {
+  const std::vector<const void*> bufs = {e->weights.p, e->x.p,   e->y.p,      e->qkv.p,
+                                         e->ctx.p,     e->ffn.p, e->slab.p,   e->io_out.p,
+                                         e->io_ids,    e->io_mask};
+  mq_encoder::Graph* hit = nullptr;
+  for (auto& g : e->graphs)
+    if (g.B == B && g.L == L && g.precision == e->precision && g.bufs == bufs) hit = &g;
+  if (!hit) {
+    if (!e->cap_stream) MQ_HIP(hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking));
+    // drop graphs that reference freed buffers, then the least recently used
+    for (size_t i = 0; i < e->graphs.size();) {
+      if (e->graphs[i].bufs != bufs) {
+        (void)hipGraphExecDestroy(e->graphs[i].exec);
+        e->graphs.erase(e->graphs.begin() + i);
+      } else {
+        ++i;
+      }
+    }
+    if (e->graphs.size() >= kMaxGraphs) {
+      auto lru = std::min_element(e->graphs.begin(), e->graphs.end(),
+                                  [](const auto& a, const auto& b) { return a.last_use < b.last_use; });
+      (void)hipGraphExecDestroy(lru->exec);
+      e->graphs.erase(lru);
+    }
+    hipGraph_t graph = nullptr;
+    MQ_HIP(hipStreamBeginCapture(e->cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = forward(e, e->io_ids, e->io_mask, B, L, e->io_out.p, e->cap_stream);
+    const hipError_t end = hipStreamEndCapture(e->cap_stream, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (end != hipSuccess) MQ_FAIL(MQ_EHIP, "graph capture failed: %s", hipGetErrorString(end));
+    mq_encoder::Graph g;
+    g.B = B;
+    g.L = L;
+    g.precision = e->precision;
+    g.bufs = bufs;
+    const hipError_t inst = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (inst != hipSuccess) MQ_FAIL(MQ_EHIP, "graph instantiate failed: %s", hipGetErrorString(inst));
+    e->graphs.push_back(g);
+    hit = &e->graphs.back();
+  }
+  hit->last_use = ++e->graph_clock;
+  MQ_HIP(hipGraphLaunch(hit->exec, s));
+  return MQ_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int64_t mq_encoder_weight_count(const mq_bert_config* cfg) {
@@ -732,6 +811,8 @@ int mq_encoder_destroy(mq_encoder* e) {
       b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
+    for (auto& g : e->graphs) (void)hipGraphExecDestroy(g.exec);
+    if (e->cap_stream) (void)hipStreamDestroy(e->cap_stream);
   }
   delete e;
   return MQ_OK;
@@ -835,6 +916,14 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   return MQ_OK;
 }
 
+int mq_encoder_set_graphs(mq_encoder* e, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(e, "NULL encoder");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->use_graphs = enabled != 0;
+  return MQ_OK;
+}
+
 int mq_encoder_set_timing(mq_encoder* e, int enabled) {
   clear_error();
   MQ_CHECK_ARG(e, "NULL encoder");
@@ -880,10 +969,11 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
     rc = bn.first->ensure(bn.second);
     if (rc) return rc;
   }
+  const bool graph = e->use_graphs && !e->tl.on;
   const int* dids = ids;
   const int* dmask = mask;
   float* dout = out;
-  if (!io_on_device) {
+  if (!io_on_device || graph) {  // stage through the encoder's own io buffers
     if (e->io_tokens < M) {
       if (e->io_ids) (void)hipFree(e->io_ids);
       if (e->io_mask) (void)hipFree(e->io_mask);
@@ -896,19 +986,21 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
     }
     rc = e->io_out.ensure((size_t)B * c.hidden);
     if (rc) return rc;
-    MQ_HIP(hipMemcpyAsync(e->io_ids, ids, M * 4, hipMemcpyHostToDevice, s));
-    MQ_HIP(hipMemcpyAsync(e->io_mask, mask, M * 4, hipMemcpyHostToDevice, s));
+    const hipMemcpyKind kind = io_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    MQ_HIP(hipMemcpyAsync(e->io_ids, ids, M * 4, kind, s));
+    MQ_HIP(hipMemcpyAsync(e->io_mask, mask, M * 4, kind, s));
     dids = e->io_ids;
     dmask = e->io_mask;
     dout = e->io_out.p;
   }
-  switch (c.hidden) {
-    case 256: rc = forward_vpl<1>(e, dids, dmask, B, L, dout, s); break;
-    case 512: rc = forward_vpl<2>(e, dids, dmask, B, L, dout, s); break;
-    case 768: rc = forward_vpl<3>(e, dids, dmask, B, L, dout, s); break;
-    default: rc = forward_vpl<4>(e, dids, dmask, B, L, dout, s); break;
+  if (graph) {
+    rc = launch_graph(e, B, L, s);
+  } else {
+    rc = forward(e, dids, dmask, B, L, dout, s);
   }
   if (rc) return rc;
+  if (io_on_device && dout != out)
+    MQ_HIP(hipMemcpyAsync(out, dout, (size_t)B * c.hidden * 4, hipMemcpyDeviceToDevice, s));
   if (!io_on_device) {
     MQ_HIP(hipMemcpyAsync(out, dout, (size_t)B * c.hidden * 4, hipMemcpyDeviceToHost, s));
     MQ_HIP(hipStreamSynchronize(s));

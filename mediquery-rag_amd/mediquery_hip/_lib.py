@@ -74,6 +74,7 @@ SIGNATURES = {
     "mq_encoder_weight_count": (_I64, [ctypes.POINTER(BertConfigC)]),
     "mq_encoder_load_weights": (_I, [_P, _P, _I64]),
     "mq_encoder_set_precision": (_I, [_P, _I]),
+    "mq_encoder_set_graphs": (_I, [_P, _I]),
     "mq_encoder_set_timing": (_I, [_P, _I]),
     "mq_encoder_read_timing": (_I, [_P, _P, _I]),
     "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),

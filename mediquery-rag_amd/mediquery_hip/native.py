@@ -173,6 +173,10 @@ class Encoder:
     def set_precision(self, dtype):
         _lib.call("mq_encoder_set_precision", self._h, dtype)
 
+    def set_graphs(self, enabled=True):
+        """Replay forwards as captured hipGraphs (default on; bit-identical results)."""
+        _lib.call("mq_encoder_set_graphs", self._h, int(bool(enabled)))
+
     def embed(self, ids, mask):
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         mask = np.ascontiguousarray(mask, dtype=np.int32)

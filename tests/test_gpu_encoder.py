@@ -79,6 +79,38 @@ def test_device_path_and_batch_invariance(require_gpu):
     np.testing.assert_allclose(enc.embed(ids[7:8], mask[7:8])[0], host[7], atol=1e-6)
 
 
+@pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6])
+def test_graph_replay_bit_identical(require_gpu, prec):
+    """Captured-hipGraph forwards equal eager forwards bit for bit, across shape
+    changes (more shapes than the graph cache holds), buffer growth, precision
+    switches, timing on/off, host and device paths."""
+    import torch
+    cfg = BertConfig(layers=2)
+    enc = Encoder(cfg)
+    enc.set_precision(prec)
+    rng = np.random.default_rng(8)
+    shapes = [(1, 32), (4, 17), (1, 32), (2, 8), (3, 5), (5, 9), (6, 3), (7, 2), (64, 32), (1, 32), (4, 17)]
+    dev = torch.device("cuda", 0)
+    for B, L in shapes:
+        ids = rng.integers(106, cfg.vocab_size, (B, L)).astype(np.int32)
+        mask = np.ones_like(ids)
+        mask[0, L // 2 + 1:] = 0
+        enc.set_graphs(False)
+        eager = enc.embed(ids, mask)
+        enc.set_graphs(True)
+        np.testing.assert_array_equal(enc.embed(ids, mask), eager)
+        np.testing.assert_array_equal(enc.embed(ids, mask), eager)   # replay
+        out = torch.empty((B, 768), dtype=torch.float32, device=dev)
+        enc.embed_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), eager)
+    enc.set_timing(True)       # timing forces eager launches; same numbers
+    ids = rng.integers(106, cfg.vocab_size, (2, 11)).astype(np.int32)
+    a = enc.embed(ids, np.ones_like(ids))
+    enc.set_timing(False)
+    np.testing.assert_array_equal(enc.embed(ids, np.ones_like(ids)), a)
+
+
 def test_errors(require_gpu):
     enc = Encoder(BertConfig(layers=1, max_positions=64))
     with pytest.raises(_lib.MQError, match="max_positions"):

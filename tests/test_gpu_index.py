@@ -89,6 +89,7 @@ def test_stream_kernel_overflow_rescan(require_gpu):
     s, i = ix.search(q, 20)
     assert ix.rescans == before + 1
     assert i[0].tolist() == ids.tolist()
+    np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
 
 
 def test_merge_thread_list_overflow_remerge(require_gpu):
@@ -113,7 +114,6 @@ def test_merge_thread_list_overflow_remerge(require_gpu):
     assert ix.remerges == m0 + 1
     ref = exact_scores(q[:2], c)
     assert check_topk(i[:2], s[:2], ref, 30) == []
-    np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
 
 
 def test_other_dims(require_gpu):
