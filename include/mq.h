@@ -179,11 +179,18 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
 /* ------------------------------------------------------- testing hooks ---- */
 /* One encoder GEMM on device buffers: out[M,N] = epi(A[M,K] W[N,K]^T + bias (+ resid)),
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,
- * 1 = 128x96, 2 = 128x64, 3 = 32x128, 4 = split-K (32x128 tiles + ordered slab
- * reduction; synchronous, N % 4 == 0), 5-9 = LDS-DMA variants, 10-12 = split-f32 (x6)
- * 128x128 / 128x96 / 128x64.  K % 32 == 0.  For kernel unit tests. */
+ * 1 = 128x96, 2 = 128x64, 3 = 32x128 (exact f32), 4 = split-K (32x128 tiles + ordered
+ * slab reduction; synchronous, N % 4 == 0), 5-7 = split-f32 (x6) 128x128 / 128x96 /
+ * 128x64 splitting fp32 operands while staging, 8-10 = the same on P3 operands (A and W
+ * given as mq_debug_split_p3 output), 11-13 = 8-10 writing `out` as P3 ([M][N*3/2]
+ * floats; epi != 3, N % 16 == 0).  K % 32 == 0.  For kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
+/* P3 layout of the split-f32 path: src [rows][K] f32 (row stride lds floats, K % 16 == 0)
+ * -> dst [rows][K/16][3][16] bf16 (3K/2 floats per row): per 16-wide chunk the planes
+ * x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1), round to nearest even.
+ * Device pointers, asynchronous on stream. */
+int mq_debug_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,9 @@
 //   K5 gemm (EPI_GELU)      FFN up + bias + GELU (erf or tanh)
 //   K6 gemm (EPI_RESID)     FFN down + bias + residual, then ln_kernel
 //   K7 pool_kernel          CLS / masked-mean pooling + L2 normalisation
-// All GEMMs run on the exact-fp32 MFMA core of gemm_f32.hpp.
+// All GEMMs run on the MFMA core of gemm_f32.hpp: exact fp32, or split-f32 (MQ_DTYPE_F32X6)
+// on P3 operands - weights split once per load, activations written as P3 by their
+// producers (LayerNorm, attention, the FFN-up epilogue).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -21,7 +23,6 @@
 
 #include "common.hpp"
 #include "gemm_f32.hpp"
-#include "gemm_glds.hpp"
 
 namespace mq {
 
@@ -47,13 +48,14 @@ __device__ __forceinline__ float wave_sum(float v) {
 // the last slice of the current one, so the epilogue overlaps the next tile's loads.
 // Within a round, the workgroups of one XCD (blockIdx % 8 equal) take consecutive
 // tiles, i.e. share A row panels in their L2.
-template <class T, int EPI>
+template <class T, int EPI, bool OUT3 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ resid, int ldr,
                                                          float* __restrict__ out, int ldo, int M,
                                                          int N, int K) {
+  static_assert(!OUT3 || (T::X6 && EPI != EPI_RESID), "P3 output: split-f32 GEMMs without residual");
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
@@ -67,11 +69,43 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     m0 = (t / tiles_n) * T::BM;
     n0 = (int64_t)(t % tiles_n) * T::BN;
   };
-  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
     int m0;
     int64_t n0l;
     coords(i, m0, n0l);
     const int n0 = (int)n0l;
+    if constexpr (OUT3) {
+      // out is P3 (row stride ldo floats): each 32x32 block goes through this wave's
+      // [32][36] image in the released stage, then lane (r, half) splits 16 consecutive
+      // values of row r and stores its 96-B P3 chunk (6 x 16 B, contiguous).
+      float* img = stage + wave * (32 * kLdsStride);
+      const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn) {
+        const int c0 = n0 + wn * T::WN + tn * 32;
+        const float b = bias[min(c0 + (lane & 31), N - 1)];
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float v = acc[tm][tn][e] + b;
+            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+            img[acc_row(0, e, lane) * kLdsStride + (lane & 31)] = v;
+          }
+          // one wave's LDS accesses complete in order: no barrier for its own image
+          floatx4 v4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v4[j] = *reinterpret_cast<const floatx4*>(img + r * kLdsStride + hf * 16 + 4 * j);
+          const int row = m0 + wm * T::WM + tm * 32 + r, col = c0 + hf * 16;
+          if (row < M && col < N)
+            split_chunk_p3(v4, reinterpret_cast<uintx4*>(out + (int64_t)row * ldo + (col >> 4) * 24));
+        }
+      }
+      __syncthreads();  // the stage is refilled after the next slice
+      return;
+    }
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn) {
       const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
@@ -91,53 +125,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
         }
     }
   };
-  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
-}
-
-// Same GEMM on the LDS-DMA core (gemm_glds.hpp): NS-stage ring, no staging VGPRs.
-template <class T, int EPI>
-__global__ __launch_bounds__(T::THREADS, T::BLOCKS_PER_CU * T::WAVES / 4) void gemm_dma_kernel(
-    const float* __restrict__ A, int lda, const float* __restrict__ W,
-    const float* __restrict__ bias, const float* __restrict__ resid, int ldr,
-    float* __restrict__ out, int ldo, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) float lds[T::LDS_FLOATS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
-  const int tiles_n = (N + T::BN - 1) / T::BN;
-  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
-  const int G = gridDim.x, per_xcd = G >> 3;
-  const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
-  auto coords = [&](int i, int& m0, int64_t& n0) {
-    const int t = i * G + xslot;
-    m0 = (t / tiles_n) * T::BM;
-    n0 = (int64_t)(t % tiles_n) * T::BN;
-  };
-  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
-    int m0;
-    int64_t n0l;
-    coords(i, m0, n0l);
-    const int n0 = (int)n0l;
-#pragma unroll
-    for (int tn = 0; tn < T::TN; ++tn) {
-      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
-      if (col >= N) continue;
-      const float b = bias[col];
-#pragma unroll
-      for (int tm = 0; tm < T::TM; ++tm)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
-          if (row >= M) continue;
-          float v = acc[tm][tn][e] + b;
-          if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-          if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-          if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
-          out[(int64_t)row * ldo + col] = v;
-        }
-    }
-  };
-  walk_tiles_dma<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
+  // P3 weights: row stride 3K/2 floats
+  const int ldw = T::P3 ? K * 3 / 2 : K;
+  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, ldw, N, K}, coords, epi);
 }
 
 // ---------------------------------------------------------- split-K GEMM ------
@@ -209,7 +199,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <int VPL>
 __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __restrict__ g,
                                              const float* __restrict__ b, float eps,
-                                             float* __restrict__ dst, int lane) {
+                                             float* __restrict__ dst, float* __restrict__ dst3,
+                                             int lane) {
   constexpr int H = VPL * 256;
   float s = 0.f;
 #pragma unroll
@@ -227,7 +218,15 @@ __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __r
     const int c = (i * 64 + lane) * 4;
     const floatx4 gg = *reinterpret_cast<const floatx4*>(g + c);
     const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c);
-    *reinterpret_cast<floatx4*>(dst + c) = x[i] * rstd * gg + bb;
+    const floatx4 y = x[i] * rstd * gg + bb;
+    *reinterpret_cast<floatx4*>(dst + c) = y;
+    if (dst3) {  // P3 copy for a split-f32 consumer: lanes 4t..4t+3 fill chunk c/16
+      uint2 pl[3];
+      split3(y, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(dst3 + (c >> 4) * 24 + p * 8 + ((c & 15) >> 1)) = pl[p];
+    }
   }
 }
 
@@ -235,7 +234,7 @@ template <int VPL>
 __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int* __restrict__ ids, int M, int L, int vocab, const float* __restrict__ word,
     const float* __restrict__ pos, const float* __restrict__ typ, const float* __restrict__ g,
-    const float* __restrict__ b, float eps, float* __restrict__ out) {
+    const float* __restrict__ b, float eps, float* __restrict__ out, float* __restrict__ out3) {
   constexpr int H = VPL * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -251,14 +250,15 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
            *reinterpret_cast<const floatx4*>(pos + (int64_t)p * H + c) +
            *reinterpret_cast<const floatx4*>(typ + c);
   }
-  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, lane);
+  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, out3 ? out3 + (int64_t)row * H * 3 / 2 : nullptr,
+                   lane);
 }
 
 template <int VPL>
 __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, int M,
                                                  const float* __restrict__ g,
                                                  const float* __restrict__ b, float eps,
-                                                 float* __restrict__ dst) {
+                                                 float* __restrict__ dst, float* __restrict__ dst3) {
   constexpr int H = VPL * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -267,7 +267,8 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 #pragma unroll
   for (int i = 0; i < VPL; ++i)
     x[i] = *reinterpret_cast<const floatx4*>(src + (int64_t)row * H + (i * 64 + lane) * 4);
-  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, lane);
+  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, dst3 ? dst3 + (int64_t)row * H * 3 / 2 : nullptr,
+                   lane);
 }
 
 // ------------------------------------------------------------ K3 attention ----
@@ -284,7 +285,8 @@ constexpr int kDh = 64;
 __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
                                                        const int* __restrict__ mask, int L,
                                                        int H, int heads, int q_tiles,
-                                                       float scale, float* __restrict__ ctx) {
+                                                       float scale, float* __restrict__ ctx,
+                                                       float* __restrict__ ctx3) {
   __shared__ float obuf[32][kDh + 1];
   const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
   const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
@@ -373,6 +375,17 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
   }
   __syncthreads();
   const int nrows = min(32, L - q0);
+  if (ctx3) {  // P3 for a split-f32 consumer: lane takes (query, 16-dim chunk) items
+    for (int it = lane; it < nrows * (kDh / 16); it += 64) {
+      const int q = it >> 2, ch = it & 3;
+      floatx4 v4[4];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v4[j >> 2][j & 3] = obuf[q][ch * 16 + j];
+      split_chunk_p3(v4, reinterpret_cast<uintx4*>(ctx3 + (row0 + q0 + q) * (H * 3 / 2) +
+                                                    ((h * kDh) >> 4) * 24 + ch * 24));
+    }
+    return;
+  }
   for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
 }
 
@@ -444,6 +457,8 @@ struct Buf {
 
 struct LayerW {
   const float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
+  // P3 copies of the four projection matrices (split-f32 path), in mq_encoder::wp3
+  const float *wqkv3 = nullptr, *wo3 = nullptr, *w13 = nullptr, *w23 = nullptr;
 };
 
 int64_t weight_count(const mq_bert_config& c) {
@@ -471,12 +486,12 @@ struct GemmArgs {
   int M, N, K;
 };
 
-template <class T, int EPI>
+template <class T, int EPI, bool OUT3 = false>
 void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s) {
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
   // persistent grid: at most two workgroups per CU, rounded up to a multiple of 8
   const int grid = (std::min(tiles, 2 * num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, OUT3>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
                      g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
 }
 
@@ -484,53 +499,34 @@ using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128
 using GemmT96 = F32Tile<4, 1, 1, 3>;    // 128 x 96
 using GemmMid = F32Tile<2, 2, 2, 1>;    // 128 x 64
 using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few rows)
-
-// Pick the tile whose launch wastes the least: every CU runs two workgroups at a time,
-// so a grid that is not a multiple of 2*CUs idles part of the chip in its last round
-// (M = 8192: N = 768 -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost model:
-// rounds * tile area / relative tile efficiency.
-template <class T, int EPI>
-void launch_gemm_dma(const GemmArgs& g, int num_cus, hipStream_t s) {
-  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-  const int grid = (std::min(tiles, T::BLOCKS_PER_CU * num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_dma_kernel<T, EPI>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda,
-                     g.W, g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
-}
-
-using DmaA = GTile<2, 2, 2, 2, 2>;  // 128x128, 4 waves, 2 stages  (2 / CU)
-using DmaB = GTile<2, 2, 2, 2, 3>;  // 128x128, 4 waves, 3 stages  (1 / CU)
-using DmaC = GTile<4, 1, 1, 3, 2>;  // 128x96,  4 waves, 2 stages  (2 / CU)
-using DmaD = GTile<4, 2, 2, 2, 3>;  // 256x128, 8 waves, 3 stages  (1 / CU)
-using DmaE = GTile<2, 4, 2, 1, 3>;  // 128x128, 8 waves (64x32), 3 stages (1 / CU)
-
-using X6Big = F32Tile<2, 2, 2, 2, true>;  // 128 x 128, split-f32
+using X6Big = F32Tile<2, 2, 2, 2, true>;  // 128 x 128, split-f32, fp32 operands split in-kernel
 using X6T96 = F32Tile<4, 1, 1, 3, true>;  // 128 x 96
 using X6Mid = F32Tile<2, 2, 2, 1, true>;  // 128 x 64
+using P3Big = F32Tile<2, 2, 2, 2, true, 2, false, true>;  // 128 x 128, split-f32, P3 operands
+using P3T96 = F32Tile<4, 1, 1, 3, true, 2, false, true>;  // 128 x 96
+using P3Mid = F32Tile<2, 2, 2, 1, true, 2, false, true>;  // 128 x 64
 
+// Tile codes (also the mq_debug_gemm_f32 `tile` argument):
+//   0-3 exact f32 128x128 / 128x96 / 128x64 / 32x128, 4 split-K (host path only),
+//   5-7 split-f32 with the split in the staging (fp32 operands), same three geometries,
+//   8-10 split-f32 on P3 operands (A and W pre-split), 11-13 the same with a P3 output.
 template <int EPI>
 void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
+  constexpr bool kP3Out = EPI != EPI_RESID;
   switch (tile) {
-    case 10: launch_gemm_t<X6Big, EPI>(g, num_cus, s); return;
-    case 11: launch_gemm_t<X6T96, EPI>(g, num_cus, s); return;
-    case 12: launch_gemm_t<X6Mid, EPI>(g, num_cus, s); return;
-    case 13: launch_gemm_t<F32Tile<2, 2, 2, 2, true, 3>, EPI>(g, num_cus, s); return;
-    case 14: launch_gemm_t<F32Tile<2, 2, 2, 2, true, 4>, EPI>(g, num_cus, s); return;
-    case 15: launch_gemm_t<F32Tile<4, 1, 1, 3, true, 3>, EPI>(g, num_cus, s); return;
-    case 16: launch_gemm_t<F32Tile<4, 1, 1, 3, true, 4>, EPI>(g, num_cus, s); return;
-    case 17: launch_gemm_t<F32Tile<4, 1, 1, 3, false, 3>, EPI>(g, num_cus, s); return;
-    case 18: launch_gemm_t<F32Tile<2, 2, 2, 2, false, 3>, EPI>(g, num_cus, s); return;
-    case 5: launch_gemm_dma<DmaA, EPI>(g, num_cus, s); return;
-    case 6: launch_gemm_dma<DmaB, EPI>(g, num_cus, s); return;
-    case 7: launch_gemm_dma<DmaC, EPI>(g, num_cus, s); return;
-    case 8: launch_gemm_dma<DmaD, EPI>(g, num_cus, s); return;
-    case 9: launch_gemm_dma<DmaE, EPI>(g, num_cus, s); return;
-    default: break;
-  }
-  switch (tile) {
-    case 0: launch_gemm_t<GemmBig, EPI>(g, num_cus, s); break;
-    case 1: launch_gemm_t<GemmT96, EPI>(g, num_cus, s); break;
-    case 2: launch_gemm_t<GemmMid, EPI>(g, num_cus, s); break;
-    default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); break;
+    case 0: launch_gemm_t<GemmBig, EPI>(g, num_cus, s); return;
+    case 1: launch_gemm_t<GemmT96, EPI>(g, num_cus, s); return;
+    case 2: launch_gemm_t<GemmMid, EPI>(g, num_cus, s); return;
+    case 5: launch_gemm_t<X6Big, EPI>(g, num_cus, s); return;
+    case 6: launch_gemm_t<X6T96, EPI>(g, num_cus, s); return;
+    case 7: launch_gemm_t<X6Mid, EPI>(g, num_cus, s); return;
+    case 8: launch_gemm_t<P3Big, EPI>(g, num_cus, s); return;
+    case 9: launch_gemm_t<P3T96, EPI>(g, num_cus, s); return;
+    case 10: launch_gemm_t<P3Mid, EPI>(g, num_cus, s); return;
+    case 11: if constexpr (kP3Out) launch_gemm_t<P3Big, EPI, kP3Out>(g, num_cus, s); return;
+    case 12: if constexpr (kP3Out) launch_gemm_t<P3T96, EPI, kP3Out>(g, num_cus, s); return;
+    case 13: if constexpr (kP3Out) launch_gemm_t<P3Mid, EPI, kP3Out>(g, num_cus, s); return;
+    default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); return;
   }
 }
 
@@ -559,30 +555,10 @@ void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
                      s, g.slab, S, g.M, g.N, g.bias, g.resid, g.ldr, g.out, g.ldo);
 }
 
-template <int EPI>
-void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false) {
-  const int S = splitk_factor(g, num_cus);
-  if (S) {
-    launch_splitk<EPI>(g, S, s);
-    return;
-  }
-  if (x6) {  // split-f32 tiles: same waste model over 128x{128,96,64}
-    const int bns[3] = {128, 96, 64};
-    const double effs[3] = {1.0, 0.96, 0.9};
-    const int64_t slots = 2 * (int64_t)num_cus;
-    int best = 0;
-    double best_cost = 1e300;
-    for (int i = 0; i < 3; ++i) {
-      const int64_t tiles = (int64_t)((g.M + 127) / 128) * ((g.N + bns[i] - 1) / bns[i]);
-      const double cost = (double)((tiles + slots - 1) / slots) * 128 * bns[i] / effs[i];
-      if (cost < best_cost) {
-        best_cost = cost;
-        best = i;
-      }
-    }
-    launch_gemm_tile<EPI>(g, 10 + best, num_cus, s);
-    return;
-  }
+// Geometry with the least waste: every CU runs two workgroups at a time, so a grid that
+// is not a multiple of 2*CUs idles part of the chip in its last round (M = 8192: N = 768
+// -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost: rounds * area / efficiency.
+int pick_tile(const GemmArgs& g, int num_cus, bool x6) {
   struct Cand {
     int bm, bn;
     double eff;
@@ -591,7 +567,7 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false)
   const int64_t slots = 2 * (int64_t)num_cus;
   int best = 0;
   double best_cost = 1e300;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < (x6 ? 3 : 4); ++i) {
     const int64_t tiles = (int64_t)((g.M + cands[i].bm - 1) / cands[i].bm) * ((g.N + cands[i].bn - 1) / cands[i].bn);
     const int64_t rounds = (tiles + slots - 1) / slots;
     const double cost = (double)rounds * cands[i].bm * cands[i].bn / cands[i].eff;
@@ -600,7 +576,26 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false)
       best = i;
     }
   }
-  launch_gemm_tile<EPI>(g, best, num_cus, s);
+  return best;
+}
+
+// Does this GEMM run on the split-f32 P3 path?  (Not when it is split-K: that path is
+// exact f32 on fp32 operands.)
+bool gemm_uses_p3(const GemmArgs& g, int num_cus, int precision) {
+  return precision == MQ_DTYPE_F32X6 && splitk_factor(g, num_cus) == 0;
+}
+
+// out = epi(A W^T + b (+ resid)).  p3 = the P3 path: A and W are P3, and with out3 the
+// output is written as P3 (not with a residual).
+template <int EPI>
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool p3 = false, bool out3 = false) {
+  const int S = splitk_factor(g, num_cus);
+  if (S) {
+    launch_splitk<EPI>(g, S, s);
+    return;
+  }
+  const int t = pick_tile(g, num_cus, p3);
+  launch_gemm_tile<EPI>(g, p3 ? (out3 ? 11 : 8) + t : t, num_cus, s);
 }
 
 // Stage labels for the optional per-kernel-class event timeline.
@@ -618,6 +613,9 @@ struct mq_encoder {
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
   Buf x, y, qkv, ctx, ffn, io_out, slab;
+  // split-f32 path: P3 weights (converted once per load) and P3 activations
+  Buf wp3, xp, ctxp, ffnp;
+  bool wp3_ready = false;
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -641,9 +639,36 @@ struct mq_encoder {
 namespace {
 
 template <int EPI>
-void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
+void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s, bool p3 = false,
+          bool out3 = false) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6);
+  launch_gemm<EPI>(g, e->num_cus, s, p3, out3);
+}
+
+// Split the four projection matrices of every layer into P3 (once per weight load).
+int ensure_p3_weights(mq_encoder* e, hipStream_t s) {
+  if (e->wp3_ready) return MQ_OK;
+  const int64_t H = e->cfg.hidden, F = e->cfg.ffn;
+  const int64_t per_layer = (3 * H * H + H * H + F * H + H * F) * 3 / 2;
+  int rc = e->wp3.ensure((size_t)(per_layer * e->layers.size()));
+  if (rc) return rc;
+  float* p = e->wp3.p;
+  for (LayerW& w : e->layers) {
+    auto split = [&](const float* src, int64_t rows, int64_t k) {
+      launch_split_p3(src, k, rows, (int)k, p, s);
+      const float* r = p;
+      p += rows * k * 3 / 2;
+      return r;
+    };
+    w.wqkv3 = split(w.wqkv, 3 * H, H);
+    w.wo3 = split(w.wo, H, H);
+    w.w13 = split(w.w1, F, H);
+    w.w23 = split(w.w2, H, F);
+  }
+  MQ_HIP(hipGetLastError());
+  MQ_HIP(hipStreamSynchronize(s));
+  e->wp3_ready = true;
+  return MQ_OK;
 }
 
 // One forward.  With CLS pooling the last layer only needs the CLS rows after its
@@ -655,12 +680,20 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
                 hipStream_t s) {
   const mq_bert_config& c = e->cfg;
   const int M = B * L, H = c.hidden, F = c.ffn;
+  const int H3 = H * 3 / 2, F3 = F * 3 / 2;  // P3 row strides in floats
   const unsigned row_blocks = (unsigned)((M + 3) / 4);
   const float scale = 1.0f / sqrtf((float)(H / c.heads));
   const int q_tiles = (L + 31) / 32;
+  // which GEMMs run split-f32 on P3 operands; their producers then write P3 copies
+  auto p3 = [&](int m, int n, int k) {
+    const GemmArgs g{e->slab.p, e->slab.n, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, m, n, k};
+    return gemm_uses_p3(g, e->num_cus, e->precision);
+  };
+  bool qkv_p3 = p3(M, 3 * H, H);
   e->tl.mark(s, ST_EMBED);
   hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, ids, M, L,
-                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p);
+                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p,
+                     qkv_p3 ? e->xp.p : nullptr);
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
     const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
@@ -668,27 +701,50 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
     const unsigned rb = (unsigned)((rows + 3) / 4);
-    gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
-                   ST_QKV, s);
+    const bool o_p3 = p3(rows, H, H), up_p3 = p3(rows, F, H), down_p3 = p3(rows, H, F);
+    const bool next_qkv_p3 = li + 1 < e->layers.size() && p3(M, 3 * H, H);
+    if (qkv_p3)
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->xp.p, H3, w.wqkv3, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+                     ST_QKV, s, true);
+    else
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+                     ST_QKV, s);
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p);
+                       H, c.heads, qt, scale, e->ctx.p, o_p3 ? e->ctxp.p : nullptr);
     // y = x + ctx Wo^T + bo  (compact [rows, H])
-    gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
-                    ST_OPROJ, s);
+    if (o_p3)
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctxp.p, cls_only ? L * H3 : H3, w.wo3, w.bo, e->x.p, stride,
+                          e->y.p, H, rows, H, H}, ST_OPROJ, s, true);
+    else
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
+                      ST_OPROJ, s);
     e->tl.mark(s, ST_LN);
     hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln1g, w.ln1b,
-                       c.ln_eps, e->x.p);
-    const GemmArgs up{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
+                       c.ln_eps, e->x.p, up_p3 ? e->xp.p : nullptr);
+    // FFN up: GELU output straight to P3 when both FFN GEMMs run split-f32
+    const bool ffn3 = up_p3 && down_p3;
+    const GemmArgs up = up_p3
+        ? GemmArgs{e->slab.p, e->slab.n, e->xp.p, H3, w.w13, w.b1, nullptr, 0, ffn3 ? e->ffnp.p : e->ffn.p,
+                   ffn3 ? F3 : F, rows, F, H}
+        : GemmArgs{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
     if (c.gelu == MQ_GELU_TANH)
-      gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s);
+      gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s, up_p3, ffn3);
     else
-      gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
-    gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F}, ST_FFN_DOWN, s);
+      gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s, up_p3, ffn3);
+    if (down_p3) {
+      if (!ffn3) launch_split_p3(e->ffn.p, F, rows, F, e->ffnp.p, s);
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffnp.p, F3, w.w23, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
+                      ST_FFN_DOWN, s, true);
+    } else {
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
+                      ST_FFN_DOWN, s);
+    }
     e->tl.mark(s, ST_LN);
     hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln2g, w.ln2b,
-                       c.ln_eps, e->x.p);
+                       c.ln_eps, e->x.p, next_qkv_p3 ? e->xp.p : nullptr);
+    qkv_p3 = next_qkv_p3;
   }
   e->tl.mark(s, ST_POOL);
   const bool pruned = c.pooling == MQ_POOL_CLS;  // x holds [B, H] CLS rows
@@ -718,9 +774,10 @@ constexpr size_t kMaxGraphs = 6;
 // Replay the forward io_ids/io_mask -> io_out for (B, L) as one hipGraph launch on s,
 // capturing it first if no cached graph matches the shape, precision and buffers.
 int launch_graph(mq_encoder* e, int B, int L, hipStream_t s) {
-  const std::vector<const void*> bufs = {e->weights.p, e->x.p,   e->y.p,      e->qkv.p,
-                                         e->ctx.p,     e->ffn.p, e->slab.p,   e->io_out.p,
-                                         e->io_ids,    e->io_mask};
+  const std::vector<const void*> bufs = {e->weights.p, e->x.p,    e->y.p,      e->qkv.p,
+                                         e->ctx.p,     e->ffn.p,  e->slab.p,   e->io_out.p,
+                                         e->io_ids,    e->io_mask, e->wp3.p,    e->xp.p,
+                                         e->ctxp.p,    e->ffnp.p};
   mq_encoder::Graph* hit = nullptr;
   for (auto& g : e->graphs)
     if (g.B == B && g.L == L && g.precision == e->precision && g.bufs == bufs) hit = &g;
@@ -807,7 +864,8 @@ int mq_encoder_destroy(mq_encoder* e) {
   if (!e) return MQ_OK;
   {
     DeviceGuard dg(e->device);
-    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab})
+    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab,
+                   &e->wp3, &e->xp, &e->ctxp, &e->ffnp})
       b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
@@ -860,6 +918,7 @@ int mq_encoder_load_weights(mq_encoder* e, const float* blob, int64_t n_floats) 
     e->layers.push_back(w);
   }
   e->loaded = true;
+  e->wp3_ready = false;  // P3 weights are re-split at the next split-f32 forward
   return MQ_OK;
 }
 
@@ -878,12 +937,17 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 18, "bad epi/tile");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 13, "bad epi/tile");
+  MQ_CHECK_ARG(tile < 11 || (epi != EPI_RESID && N % 16 == 0), "P3 output: no residual, N %% 16 == 0");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   GemmArgs g{nullptr, 0, A, K, W, bias, resid, N, out, N, M, N, K};
   hipStream_t s = (hipStream_t)stream;
+  if (tile >= 8) {  // A and W are P3 (mq_debug_split_p3); tiles 11-13 write `out` as P3
+    g.lda = K * 3 / 2;
+    if (tile >= 11) g.ldo = N * 3 / 2;
+  }
   if (tile == 4) {  // split-K path (test hook: allocates its own slab)
     MQ_CHECK_ARG(N % 4 == 0, "split-K needs N %% 4 == 0");
     const int slices = K / kBK;
@@ -912,6 +976,14 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
     case EPI_GELU_TANH: launch_gemm_tile<EPI_GELU_TANH>(g, tile, cus, s); break;
     default: launch_gemm_tile<EPI_RESID>(g, tile, cus, s); break;
   }
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_debug_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(src && dst && rows >= 0 && K > 0 && K % 16 == 0 && lds >= K, "bad split_p3 arguments");
+  launch_split_p3(src, lds, rows, K, dst, (hipStream_t)stream);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -967,6 +1039,15 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
                   std::make_pair(&e->ffn, M * c.ffn)}) {
     rc = bn.first->ensure(bn.second);
+    if (rc) return rc;
+  }
+  if (e->precision == MQ_DTYPE_F32X6) {  // P3 activations + weights of the split-f32 path
+    for (auto bn : {std::make_pair(&e->xp, M * c.hidden * 3 / 2), std::make_pair(&e->ctxp, M * c.hidden * 3 / 2),
+                    std::make_pair(&e->ffnp, M * c.ffn * 3 / 2)}) {
+      rc = bn.first->ensure(bn.second);
+      if (rc) return rc;
+    }
+    rc = ensure_p3_weights(e, s);
     if (rc) return rc;
   }
   const bool graph = e->use_graphs && !e->tl.on;

@@ -84,7 +84,7 @@ struct TopList {
 
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
-using SearchWideX6 = F32Tile<2, 2, 2, 2, true>;  // same, split-f32 arithmetic
+using SearchWideX6 = F32Tile<2, 2, 2, 2, true, 2, false, true>;  // split-f32 on P3 operands
 using SearchWideBF = F32Tile<2, 2, 2, 2, false, 2, true>;    // bf16 coarse scan
 using SearchNarrowBF = F32Tile<1, 4, 1, 1, false, 2, true>;  // bf16 coarse, small batches
 using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
@@ -168,7 +168,8 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
       __syncthreads();
     }
   };
-  walk_tiles<T>(lds, n_tiles, TileOperands{Q, dim, nq, C, dim, n_rows, dim}, coords, epi);
+  const int ld = T::P3 ? dim * 3 / 2 : dim;  // P3 rows: 3*dim/2 floats
+  walk_tiles<T>(lds, n_tiles, TileOperands{Q, ld, nq, C, ld, n_rows, dim}, coords, epi);
 
   const int list = (g * T::WAVES_N + wn) * S::LPQ + part;
   const int qg = m0 + wm * T::WM + q_local;
@@ -525,6 +526,9 @@ struct mq_index {
   DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
   int64_t n16 = 0;   // rows already mirrored into rows16
   DevBuf q16, coarse_s, coarse_i;
+  DevBuf rows3;      // P3 shadow of `rows` for the split-f32 scan ([cap, 3*dim/2] floats)
+  int64_t n3 = 0;    // rows already mirrored into rows3
+  DevBuf q3;         // P3 copy of the query batch
   DevBuf flag;          // merge overflow flag (k > 16)
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
   int64_t remerges = 0;  // merges re-run with 64-entry thread lists
@@ -539,8 +543,9 @@ namespace {
 template <class T, int KC>
 void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int nqt,
                    float* cs, int* ci, hipStream_t s) {
-  // bf16 tiles read the bf16 shadow as float-typed rows of half the width
-  const float* rows = T::BF16 ? ix->rows16.as<float>() : ix->rows;
+  // bf16 tiles read the bf16 shadow as float-typed rows of half the width; split-f32
+  // tiles the P3 shadow (and P3 queries)
+  const float* rows = T::BF16 ? ix->rows16.as<float>() : (T::P3 ? ix->rows3.as<float>() : ix->rows);
   const int dim = T::BF16 ? ix->dim / 2 : ix->dim;
   hipLaunchKernelGGL((flat_search_kernel<T, KC>), dim3(G * nqt), dim3(256), 0, s, q, nq, rows,
                      ix->n, dim, G, nqt, k, cs, ci);
@@ -634,8 +639,8 @@ int stream_blocks(const mq_index* ix) {
 }
 
 template <int KC>
-void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq, int kl, int G,
-                 int nqt, float* cs, int* ci, hipStream_t s) {
+void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, const float* q3, int nq,
+                 int kl, int G, int nqt, float* cs, int* ci, hipStream_t s) {
   if (kind == SCAN_BF16) {
     if (wide)
       launch_search<SearchWideBF, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
@@ -644,8 +649,8 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq
     return;
   }
   if constexpr (KC <= 16) {  // (a 64-entry list spills next to the x6 operands)
-    if (kind == SCAN_X6 && wide) {
-      launch_search<SearchWideX6, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
+    if (kind == SCAN_X6 && wide && q3) {
+      launch_search<SearchWideX6, KC>(ix, q3, nq, kl, G, nqt, cs, ci, s);
       return;
     }
   }
@@ -661,7 +666,7 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq
 // batch is re-scanned with 64-entry lists, so results are exact either way.  The
 // check costs one 4-byte device->host read, i.e. k > 16 calls are synchronous.
 int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* os, int64_t* oi,
-              hipStream_t s) {
+              hipStream_t s, const float* q3 = nullptr) {
   int kc = kc_scan(k);
   for (;;) {
     const int kl = std::min(kc, k);
@@ -687,9 +692,9 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
         default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
       }
     } else switch (kc) {
-      case 8: launch_scan<8>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
-      case 16: launch_scan<16>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
-      default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      case 8: launch_scan<8>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      case 16: launch_scan<16>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
     }
     MQ_HIP(hipGetLastError());
     ix->tl.mark(s, 1);
@@ -757,7 +762,22 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
-  return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
+  if (ix->precision == MQ_DTYPE_F32X6 && nq > 64 && ix->dim % 16 == 0) {
+    // split-f32 scan on P3 operands: mirror rows added since the last one, split queries
+    const int64_t w3 = (int64_t)ix->dim * 3 / 2;
+    int rc = ix->rows3.ensure((size_t)ix->cap * w3 * sizeof(float));
+    if (!rc) rc = ix->q3.ensure((size_t)nq * w3 * sizeof(float));
+    if (rc) return rc;
+    if (ix->n3 < ix->n) {
+      launch_split_p3(ix->rows + ix->n3 * ix->dim, ix->dim, ix->n - ix->n3, ix->dim,
+                      ix->rows3.as<float>() + ix->n3 * w3, s);
+      ix->n3 = ix->n;
+    }
+    launch_split_p3(q, ix->dim, nq, ix->dim, ix->q3.as<float>(), s);
+    MQ_HIP(hipGetLastError());
+    return scan_topk(ix, SCAN_X6, q, nq, k, os, oi, s, ix->q3.as<float>());
+  }
+  return scan_topk(ix, SCAN_F32, q, nq, k, os, oi, s);
 }
 
 int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
@@ -775,7 +795,8 @@ int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
   if (ix->rows) MQ_HIP(hipFree(ix->rows));
   ix->rows = fresh;
   ix->cap = new_cap;
-  ix->n16 = 0;  // the bf16 shadow is rebuilt at the next coarse search
+  ix->n16 = 0;  // the bf16 / P3 shadows are rebuilt at the next search that needs them
+  ix->n3 = 0;
   return MQ_OK;
 }
 
@@ -831,6 +852,8 @@ int mq_index_destroy(mq_index* ix) {
     ix->out_i.release();
     ix->rows16.release();
     ix->q16.release();
+    ix->rows3.release();
+    ix->q3.release();
     ix->coarse_s.release();
     ix->coarse_i.release();
     ix->flag.release();
@@ -866,6 +889,7 @@ int mq_index_reset(mq_index* ix) {
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->n = 0;
   ix->n16 = 0;
+  ix->n3 = 0;
   return MQ_OK;
 }
 
@@ -1042,6 +1066,7 @@ int mq_index_load(mq_index* ix, const char* path) {
   }
   ix->n = 0;
   ix->n16 = 0;
+  ix->n3 = 0;
   int rc = reserve_rows(ix, h.n_rows, nullptr);
   if (rc) {
     fclose(f);

@@ -84,6 +84,7 @@ SIGNATURES = {
     "mq_tokenizer_encode_batch": (_I, [_P, ctypes.POINTER(ctypes.c_char_p), _I, _I, _P, _P,
                                        ctypes.POINTER(_I)]),
     "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mq_debug_split_p3": (_I, [_P, _I64, _I64, _I, _P, _P]),
 }
 
 _lib = None
