@@ -183,7 +183,9 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
  * slab reduction; synchronous, N % 4 == 0), 5-7 = split-f32 (x6) 128x128 / 128x96 /
  * 128x64 splitting fp32 operands while staging, 8-10 = the same on P3 operands (A and W
  * given as mq_debug_split_p3 output), 11-13 = 8-10 writing `out` as P3 ([M][N*3/2]
- * floats; epi != 3, N % 16 == 0).  K % 32 == 0.  For kernel unit tests. */
+ * floats; epi != 3, N % 16 == 0), 14 / 15 = the wide 8-wave split-f32 kernel 256x96 /
+ * 256x128 on P3T operands (mq_debug_split_p3t output), 16 / 17 = 14 / 15 writing `out`
+ * as P3T (epi != 3, N % 16 == 0).  K % 32 == 0.  For kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
 /* P3 layout of the split-f32 path: src [rows][K] f32 (row stride lds floats, K % 16 == 0)
@@ -191,6 +193,11 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
  * x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1), round to nearest even.
  * Device pointers, asynchronous on stream. */
 int mq_debug_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream);
+/* Tiled P3 (P3T) of the wide split-f32 kernel: the same planes as P3, stored as 1-KiB
+ * pieces (row block of 32, 16-wide k-chunk, plane) = [h][32 rows][8 bf16], piece
+ * (rb, c, p) at float offset ((rb * K/16 + c) * 3 + p) * 256; rows padded to a multiple
+ * of 32 with copies of the last row: dst holds ceil(rows/32)*32 * 3K/2 floats. */
+int mq_debug_split_p3t(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "gemm_f32.hpp"
+#include "gemm_x6w.hpp"
 
 namespace mq {
 
@@ -130,6 +131,81 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
   walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, ldw, N, K}, coords, epi);
 }
 
+// Wide split-f32 GEMM (gemm_x6w.hpp): A3 [M][K] and W3 [N][K] in P3T, one 8-wave
+// workgroup per CU walking tiles; out fp32 (row stride ldo) or, with OUT3, P3T with N
+// columns.  Same epilogues as gemm_nt_kernel.
+template <class T, int EPI, bool OUT3 = false>
+__global__ __launch_bounds__(T::THREADS, 1) void gemm_wide_kernel(const float* __restrict__ A3,
+                                                                  const float* __restrict__ W3,
+                                                                  const float* __restrict__ bias,
+                                                                  const float* __restrict__ resid,
+                                                                  int ldr, float* __restrict__ out,
+                                                                  int ldo, int M, int N, int K) {
+  static_assert(!OUT3 || EPI != EPI_RESID, "P3T output without residual");
+  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  const int tiles_n = (N + T::BN - 1) / T::BN;
+  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
+  const int G = gridDim.x, per_xcd = G >> 3;
+  const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
+  auto coords = [&](int i, int& m0, int& n0) {
+    const int t = i * G + xslot;
+    m0 = (t / tiles_n) * T::BM;
+    n0 = (t % tiles_n) * T::BN;
+  };
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
+    int m0, n0;
+    coords(i, m0, n0);
+    if constexpr (OUT3) {
+      float* img = stage + wave * (32 * kLdsStride);
+      const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn) {
+        const int c0 = n0 + wn * T::WN + tn * 32;
+        const float b = bias[min(c0 + (lane & 31), N - 1)];
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float v = acc[tm][tn][e] + b;
+            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+            img[acc_row(0, e, lane) * kLdsStride + (lane & 31)] = v;
+          }
+          floatx4 v4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v4[j] = *reinterpret_cast<const floatx4*>(img + r * kLdsStride + hf * 16 + 4 * j);
+          const int row = m0 + wm * T::WM + tm * 32 + r, col = c0 + hf * 16;
+          if (row < M && col < N) p3t_store16(out, row, col, N, v4);
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn) {
+      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float b = bias[col];
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
+          if (row >= M) continue;
+          float v = acc[tm][tn][e] + b;
+          if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+          if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+          if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+          out[(int64_t)row * ldo + col] = v;
+        }
+    }
+  };
+  walk_tiles_wide<T>(lds, n_tiles, WideOperands{A3, M, W3, N, K}, coords, epi);
+}
+
 // ---------------------------------------------------------- split-K GEMM ------
 // For few rows (single queries, the CLS-only last layer) the direct GEMM leaves most
 // CUs idle.  Split K into S chunks: workgroup (tile, s) multiplies its tile over
@@ -200,7 +276,7 @@ template <int VPL>
 __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __restrict__ g,
                                              const float* __restrict__ b, float eps,
                                              float* __restrict__ dst, float* __restrict__ dst3,
-                                             int lane) {
+                                             int64_t row, int lane) {
   constexpr int H = VPL * 256;
   float s = 0.f;
 #pragma unroll
@@ -220,13 +296,7 @@ __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __r
     const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c);
     const floatx4 y = x[i] * rstd * gg + bb;
     *reinterpret_cast<floatx4*>(dst + c) = y;
-    if (dst3) {  // P3 copy for a split-f32 consumer: lanes 4t..4t+3 fill chunk c/16
-      uint2 pl[3];
-      split3(y, pl);
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        *reinterpret_cast<uint2*>(dst3 + (c >> 4) * 24 + p * 8 + ((c & 15) >> 1)) = pl[p];
-    }
+    if (dst3) p3t_store4(dst3, row, c, H, y);  // P3T copy for a split-f32 consumer
   }
 }
 
@@ -250,8 +320,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
            *reinterpret_cast<const floatx4*>(pos + (int64_t)p * H + c) +
            *reinterpret_cast<const floatx4*>(typ + c);
   }
-  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, out3 ? out3 + (int64_t)row * H * 3 / 2 : nullptr,
-                   lane);
+  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, out3, row, lane);
 }
 
 template <int VPL>
@@ -267,8 +336,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 #pragma unroll
   for (int i = 0; i < VPL; ++i)
     x[i] = *reinterpret_cast<const floatx4*>(src + (int64_t)row * H + (i * 64 + lane) * 4);
-  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, dst3 ? dst3 + (int64_t)row * H * 3 / 2 : nullptr,
-                   lane);
+  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, dst3, row, lane);
 }
 
 // ------------------------------------------------------------ K3 attention ----
@@ -286,7 +354,7 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
                                                        const int* __restrict__ mask, int L,
                                                        int H, int heads, int q_tiles,
                                                        float scale, float* __restrict__ ctx,
-                                                       float* __restrict__ ctx3) {
+                                                       float* __restrict__ ctx3, int cls_compact) {
   __shared__ float obuf[32][kDh + 1];
   const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
   const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
@@ -375,14 +443,15 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
   }
   __syncthreads();
   const int nrows = min(32, L - q0);
-  if (ctx3) {  // P3 for a split-f32 consumer: lane takes (query, 16-dim chunk) items
-    for (int it = lane; it < nrows * (kDh / 16); it += 64) {
+  if (ctx3) {  // P3T for a split-f32 consumer: lane takes (query, 16-dim chunk) items;
+               // cls_compact: only the CLS row, stored as row bseq
+    const int nq = cls_compact ? 1 : nrows;
+    for (int it = lane; it < nq * (kDh / 16); it += 64) {
       const int q = it >> 2, ch = it & 3;
       floatx4 v4[4];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v4[j >> 2][j & 3] = obuf[q][ch * 16 + j];
-      split_chunk_p3(v4, reinterpret_cast<uintx4*>(ctx3 + (row0 + q0 + q) * (H * 3 / 2) +
-                                                    ((h * kDh) >> 4) * 24 + ch * 24));
+      p3t_store16(ctx3, cls_compact ? bseq : row0 + q0 + q, h * kDh + ch * 16, H, v4);
     }
     return;
   }
@@ -457,7 +526,7 @@ struct Buf {
 
 struct LayerW {
   const float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
-  // P3 copies of the four projection matrices (split-f32 path), in mq_encoder::wp3
+  // P3T copies of the four projection matrices (split-f32 path), in mq_encoder::wp3
   const float *wqkv3 = nullptr, *wo3 = nullptr, *w13 = nullptr, *w23 = nullptr;
 };
 
@@ -506,10 +575,24 @@ using P3Big = F32Tile<2, 2, 2, 2, true, 2, false, true>;  // 128 x 128, split-f3
 using P3T96 = F32Tile<4, 1, 1, 3, true, 2, false, true>;  // 128 x 96
 using P3Mid = F32Tile<2, 2, 2, 1, true, 2, false, true>;  // 128 x 64
 
+using WideA = WTile<8, 1, 1, 3, 2>;  // 256 x 96, 8 waves of 32 x 96, 32-deep stages
+using WideB = WTile<4, 2, 2, 2, 2>;  // 256 x 128, 8 waves of 64 x 64
+
+template <class T, int EPI, bool OUT3 = false>
+void launch_wide_t(const GemmArgs& g, int num_cus, hipStream_t s) {
+  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+  // persistent grid: one 8-wave workgroup per CU, a multiple of 8 (XCD remap)
+  const int grid = (std::min(tiles, num_cus) + 7) / 8 * 8;
+  hipLaunchKernelGGL((gemm_wide_kernel<T, EPI, OUT3>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.W,
+                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
+}
+
 // Tile codes (also the mq_debug_gemm_f32 `tile` argument):
 //   0-3 exact f32 128x128 / 128x96 / 128x64 / 32x128, 4 split-K (host path only),
 //   5-7 split-f32 with the split in the staging (fp32 operands), same three geometries,
-//   8-10 split-f32 on P3 operands (A and W pre-split), 11-13 the same with a P3 output.
+//   8-10 split-f32 on P3 operands (A and W pre-split), 11-13 the same with a P3 output,
+//   14 / 15 the wide 8-wave split-f32 kernel 256x96 / 256x128 on P3T operands, 16 / 17
+//   the same writing P3T.
 template <int EPI>
 void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
   constexpr bool kP3Out = EPI != EPI_RESID;
@@ -526,6 +609,10 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
     case 11: if constexpr (kP3Out) launch_gemm_t<P3Big, EPI, kP3Out>(g, num_cus, s); return;
     case 12: if constexpr (kP3Out) launch_gemm_t<P3T96, EPI, kP3Out>(g, num_cus, s); return;
     case 13: if constexpr (kP3Out) launch_gemm_t<P3Mid, EPI, kP3Out>(g, num_cus, s); return;
+    case 14: launch_wide_t<WideA, EPI>(g, num_cus, s); return;
+    case 15: launch_wide_t<WideB, EPI>(g, num_cus, s); return;
+    case 16: if constexpr (kP3Out) launch_wide_t<WideA, EPI, kP3Out>(g, num_cus, s); return;
+    case 17: if constexpr (kP3Out) launch_wide_t<WideB, EPI, kP3Out>(g, num_cus, s); return;
     default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); return;
   }
 }
@@ -585,8 +672,8 @@ bool gemm_uses_p3(const GemmArgs& g, int num_cus, int precision) {
   return precision == MQ_DTYPE_F32X6 && splitk_factor(g, num_cus) == 0;
 }
 
-// out = epi(A W^T + b (+ resid)).  p3 = the P3 path: A and W are P3, and with out3 the
-// output is written as P3 (not with a residual).
+// out = epi(A W^T + b (+ resid)).  p3 = the split-f32 path: A and W are P3T, and with
+// out3 the output is written as P3T (not with a residual).
 template <int EPI>
 void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool p3 = false, bool out3 = false) {
   const int S = splitk_factor(g, num_cus);
@@ -594,8 +681,15 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool p3 = false,
     launch_splitk<EPI>(g, S, s);
     return;
   }
-  const int t = pick_tile(g, num_cus, p3);
-  launch_gemm_tile<EPI>(g, p3 ? (out3 ? 11 : 8) + t : t, num_cus, s);
+  if (p3) {  // wide split-f32 kernel on P3T operands: 256x96 or 256x128, one WG per CU
+    const int64_t mt = (g.M + 255) / 256;
+    const int64_t ra = (mt * ((g.N + 95) / 96) + num_cus - 1) / num_cus;
+    const int64_t rb = (mt * ((g.N + 127) / 128) + num_cus - 1) / num_cus;
+    const bool wide_b = rb * 128 < ra * 96;
+    launch_gemm_tile<EPI>(g, (out3 ? 16 : 14) + (wide_b ? 1 : 0), num_cus, s);
+    return;
+  }
+  launch_gemm_tile<EPI>(g, pick_tile(g, num_cus, false), num_cus, s);
 }
 
 // Stage labels for the optional per-kernel-class event timeline.
@@ -613,7 +707,7 @@ struct mq_encoder {
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
   Buf x, y, qkv, ctx, ffn, io_out, slab;
-  // split-f32 path: P3 weights (converted once per load) and P3 activations
+  // split-f32 path: P3T weights (converted once per load) and P3T activations
   Buf wp3, xp, ctxp, ffnp;
   bool wp3_ready = false;
   int* io_ids = nullptr;
@@ -645,19 +739,20 @@ void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s, bool p3 = 
   launch_gemm<EPI>(g, e->num_cus, s, p3, out3);
 }
 
-// Split the four projection matrices of every layer into P3 (once per weight load).
+// Split the four projection matrices of every layer into P3T (once per weight load).
 int ensure_p3_weights(mq_encoder* e, hipStream_t s) {
   if (e->wp3_ready) return MQ_OK;
   const int64_t H = e->cfg.hidden, F = e->cfg.ffn;
-  const int64_t per_layer = (3 * H * H + H * H + F * H + H * F) * 3 / 2;
+  const int64_t per_layer = p3t_floats(3 * H, (int)H) + p3t_floats(H, (int)H) + p3t_floats(F, (int)H) +
+                            p3t_floats(H, (int)F);
   int rc = e->wp3.ensure((size_t)(per_layer * e->layers.size()));
   if (rc) return rc;
   float* p = e->wp3.p;
   for (LayerW& w : e->layers) {
     auto split = [&](const float* src, int64_t rows, int64_t k) {
-      launch_split_p3(src, k, rows, (int)k, p, s);
+      launch_split_p3t(src, k, rows, (int)k, p, s);
       const float* r = p;
-      p += rows * k * 3 / 2;
+      p += p3t_floats(rows, (int)k);
       return r;
     };
     w.wqkv3 = split(w.wqkv, 3 * H, H);
@@ -680,7 +775,6 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
                 hipStream_t s) {
   const mq_bert_config& c = e->cfg;
   const int M = B * L, H = c.hidden, F = c.ffn;
-  const int H3 = H * 3 / 2, F3 = F * 3 / 2;  // P3 row strides in floats
   const unsigned row_blocks = (unsigned)((M + 3) / 4);
   const float scale = 1.0f / sqrtf((float)(H / c.heads));
   const int q_tiles = (L + 31) / 32;
@@ -704,7 +798,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     const bool o_p3 = p3(rows, H, H), up_p3 = p3(rows, F, H), down_p3 = p3(rows, H, F);
     const bool next_qkv_p3 = li + 1 < e->layers.size() && p3(M, 3 * H, H);
     if (qkv_p3)
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->xp.p, H3, w.wqkv3, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->xp.p, 0, w.wqkv3, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
                      ST_QKV, s, true);
     else
       gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
@@ -712,11 +806,11 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p, o_p3 ? e->ctxp.p : nullptr);
+                       H, c.heads, qt, scale, e->ctx.p, o_p3 ? e->ctxp.p : nullptr, cls_only ? 1 : 0);
     // y = x + ctx Wo^T + bo  (compact [rows, H])
     if (o_p3)
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctxp.p, cls_only ? L * H3 : H3, w.wo3, w.bo, e->x.p, stride,
-                          e->y.p, H, rows, H, H}, ST_OPROJ, s, true);
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctxp.p, 0, w.wo3, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
+                      ST_OPROJ, s, true);
     else
       gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
                       ST_OPROJ, s);
@@ -726,16 +820,16 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     // FFN up: GELU output straight to P3 when both FFN GEMMs run split-f32
     const bool ffn3 = up_p3 && down_p3;
     const GemmArgs up = up_p3
-        ? GemmArgs{e->slab.p, e->slab.n, e->xp.p, H3, w.w13, w.b1, nullptr, 0, ffn3 ? e->ffnp.p : e->ffn.p,
-                   ffn3 ? F3 : F, rows, F, H}
+        ? GemmArgs{e->slab.p, e->slab.n, e->xp.p, 0, w.w13, w.b1, nullptr, 0, ffn3 ? e->ffnp.p : e->ffn.p,
+                   F, rows, F, H}
         : GemmArgs{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
     if (c.gelu == MQ_GELU_TANH)
       gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s, up_p3, ffn3);
     else
       gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s, up_p3, ffn3);
     if (down_p3) {
-      if (!ffn3) launch_split_p3(e->ffn.p, F, rows, F, e->ffnp.p, s);
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffnp.p, F3, w.w23, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
+      if (!ffn3) launch_split_p3t(e->ffn.p, F, rows, F, e->ffnp.p, s);
+      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffnp.p, 0, w.w23, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
                       ST_FFN_DOWN, s, true);
     } else {
       gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
@@ -937,17 +1031,18 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 13, "bad epi/tile");
-  MQ_CHECK_ARG(tile < 11 || (epi != EPI_RESID && N % 16 == 0), "P3 output: no residual, N %% 16 == 0");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 17, "bad epi/tile");
+  MQ_CHECK_ARG(!((tile >= 11 && tile <= 13) || tile >= 16) || (epi != EPI_RESID && N % 16 == 0),
+               "P3 output: no residual, N %% 16 == 0");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   GemmArgs g{nullptr, 0, A, K, W, bias, resid, N, out, N, M, N, K};
   hipStream_t s = (hipStream_t)stream;
-  if (tile >= 8) {  // A and W are P3 (mq_debug_split_p3); tiles 11-13 write `out` as P3
+  if (tile >= 8 && tile <= 13) {  // A and W are P3 (mq_debug_split_p3); 11-13 write P3
     g.lda = K * 3 / 2;
     if (tile >= 11) g.ldo = N * 3 / 2;
-  }
+  }  // 14-17: A and W are P3T (mq_debug_split_p3t); 16-17 write `out` as P3T
   if (tile == 4) {  // split-K path (test hook: allocates its own slab)
     MQ_CHECK_ARG(N % 4 == 0, "split-K needs N %% 4 == 0");
     const int slices = K / kBK;
@@ -976,6 +1071,14 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
     case EPI_GELU_TANH: launch_gemm_tile<EPI_GELU_TANH>(g, tile, cus, s); break;
     default: launch_gemm_tile<EPI_RESID>(g, tile, cus, s); break;
   }
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_debug_split_p3t(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(src && dst && rows >= 0 && K > 0 && K % 16 == 0 && lds >= K, "bad split_p3t arguments");
+  launch_split_p3t(src, lds, rows, K, dst, (hipStream_t)stream);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1042,8 +1145,9 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
     if (rc) return rc;
   }
   if (e->precision == MQ_DTYPE_F32X6) {  // P3 activations + weights of the split-f32 path
-    for (auto bn : {std::make_pair(&e->xp, M * c.hidden * 3 / 2), std::make_pair(&e->ctxp, M * c.hidden * 3 / 2),
-                    std::make_pair(&e->ffnp, M * c.ffn * 3 / 2)}) {
+    for (auto bn : {std::make_pair(&e->xp, (size_t)p3t_floats(M, c.hidden)),
+                    std::make_pair(&e->ctxp, (size_t)p3t_floats(M, c.hidden)),
+                    std::make_pair(&e->ffnp, (size_t)p3t_floats(M, c.ffn))}) {
       rc = bn.first->ensure(bn.second);
       if (rc) return rc;
     }

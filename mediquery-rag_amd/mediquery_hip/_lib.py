@@ -85,6 +85,7 @@ SIGNATURES = {
                                        ctypes.POINTER(_I)]),
     "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "mq_debug_split_p3": (_I, [_P, _I64, _I64, _I, _P, _P]),
+    "mq_debug_split_p3t": (_I, [_P, _I64, _I64, _I, _P, _P]),
 }
 
 _lib = None

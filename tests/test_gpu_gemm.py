@@ -135,3 +135,46 @@ def test_p3_operands_bit_identical(require_gpu, epi, M, N, K):
         if epi != 3 and N % 16 == 0:
             p3 = run(11 + t, torch.zeros((M, N * 3 // 2), device=dev))
             np.testing.assert_array_equal(p3.view(np.uint16).reshape(M, N // 16, 3, 16), split_p3(ref))
+
+
+def p3t_to_p3(buf, rows, K):
+    """P3T buffer (uint16 view) -> P3 planes [rows][K/16][3][16] (pad rows dropped)."""
+    rb = (rows + 31) // 32
+    x = buf.reshape(rb, K // 16, 3, 2, 32, 8).transpose(0, 4, 1, 2, 3, 5)
+    return x.reshape(rb * 32, K // 16, 3, 16)[:rows]
+
+
+@pytest.mark.parametrize("epi", [0, 1, 3])
+@pytest.mark.parametrize("M,N,K", [(77, 96, 64), (300, 2304, 768), (1000, 768, 3072), (513, 3072, 768),
+                                   (8192, 768, 768)])
+def test_wide_split_f32_bit_identical(require_gpu, epi, M, N, K):
+    """The wide 8-wave kernel on P3T operands (tiles 14 / 15) equals the 4-wave split-f32
+    tile (5) bit for bit; 16 / 17 write exactly the P3T split of that output."""
+    import torch
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(M + 5 * N + K)
+    A = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.05
+    b = torch.randn(N, device=dev, generator=g)
+    R = torch.randn(M, N, device=dev, generator=g)
+    pad = lambda r: (r + 31) // 32 * 32  # noqa: E731
+    A3 = torch.empty(pad(M) * K * 3 // 2, device=dev)
+    W3 = torch.empty(pad(N) * K * 3 // 2, device=dev)
+    _lib.call("mq_debug_split_p3t", _lib.ptr(A), K, M, K, _lib.ptr(A3), _lib.stream_handle())
+    _lib.call("mq_debug_split_p3t", _lib.ptr(W), K, N, K, _lib.ptr(W3), _lib.stream_handle())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(p3t_to_p3(A3.cpu().numpy().view(np.uint16), M, K), split_p3(A.cpu().numpy()))
+
+    def run(tile, a, w, out):
+        _lib.call("mq_debug_gemm_f32", _lib.ptr(a), _lib.ptr(w), _lib.ptr(b), _lib.ptr(R), _lib.ptr(out),
+                  M, N, K, epi, tile, _lib.stream_handle())
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    ref = run(5, A, W, torch.full((M, N), float("nan"), device=dev))
+    for tile in (14, 15):
+        got = run(tile, A3, W3, torch.full((M, N), float("nan"), device=dev))
+        np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+        if epi != 3 and N % 16 == 0:
+            buf = run(tile + 2, A3, W3, torch.zeros(pad(M) * N * 3 // 2, device=dev))
+            np.testing.assert_array_equal(p3t_to_p3(buf.view(np.uint16), M, N), split_p3(ref))
