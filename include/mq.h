@@ -85,6 +85,11 @@ int mq_index_reset(mq_index* ix);
  * 64 when a list may have dropped a top-k member), so it returns after the search. */
 int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k,
                     float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
+/* Replace dst's rows with src's rows[0..n) (host int64 row ids in [0, size(src)), any
+ * order, repeats allowed), gathered on the device - no host copy of the slab.  dst may be
+ * src (in-place compaction after a delete).  Used for Chroma-style `filter` searches
+ * and `delete` (reference VectorStore surface).  Synchronous. */
+int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst);
 /* Copy stored (normalised) rows [row0, row0 + n) into out [n, dim] f32 (host or device). */
 int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_device, void* stream);
 /* Arithmetic of the fused scan: MQ_DTYPE_F32 (default, exact), MQ_DTYPE_F32X6 (split
@@ -181,23 +186,9 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,
  * 1 = 128x96, 2 = 128x64, 3 = 32x128 (exact f32), 4 = split-K (32x128 tiles + ordered
  * slab reduction; synchronous, N % 4 == 0), 5-7 = split-f32 (x6) 128x128 / 128x96 /
- * 128x64 splitting fp32 operands while staging, 8-10 = the same on P3 operands (A and W
- * given as mq_debug_split_p3 output), 11-13 = 8-10 writing `out` as P3 ([M][N*3/2]
- * floats; epi != 3, N % 16 == 0), 14 / 15 = the wide 8-wave split-f32 kernel 256x96 /
- * 256x128 on P3T operands (mq_debug_split_p3t output), 16 / 17 = 14 / 15 writing `out`
- * as P3T (epi != 3, N % 16 == 0).  K % 32 == 0.  For kernel unit tests. */
+ * 128x64.  K % 32 == 0.  For kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
-/* P3 layout of the split-f32 path: src [rows][K] f32 (row stride lds floats, K % 16 == 0)
- * -> dst [rows][K/16][3][16] bf16 (3K/2 floats per row): per 16-wide chunk the planes
- * x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1), round to nearest even.
- * Device pointers, asynchronous on stream. */
-int mq_debug_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream);
-/* Tiled P3 (P3T) of the wide split-f32 kernel: the same planes as P3, stored as 1-KiB
- * pieces (row block of 32, 16-wide k-chunk, plane) = [h][32 rows][8 bf16], piece
- * (rb, c, p) at float offset ((rb * K/16 + c) * 3 + p) * 256; rows padded to a multiple
- * of 32 with copies of the last row: dst holds ceil(rows/32)*32 * 3K/2 floats. */
-int mq_debug_split_p3t(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream);
 
 #ifdef __cplusplus
 }

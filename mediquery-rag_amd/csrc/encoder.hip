@@ -12,18 +12,16 @@
 //   K5 gemm (EPI_GELU)      FFN up + bias + GELU (erf or tanh)
 //   K6 gemm (EPI_RESID)     FFN down + bias + residual, then ln_kernel
 //   K7 pool_kernel          CLS / masked-mean pooling + L2 normalisation
-// All GEMMs run on the MFMA core of gemm_f32.hpp: exact fp32, or split-f32 (MQ_DTYPE_F32X6)
-// on P3 operands - weights split once per load, activations written as P3 by their
-// producers (LayerNorm, attention, the FFN-up epilogue).
+// All GEMMs run on the exact-fp32 MFMA core of gemm_f32.hpp.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
 
 #include "common.hpp"
 #include "gemm_f32.hpp"
-#include "gemm_x6w.hpp"
 
 namespace mq {
 
@@ -49,14 +47,13 @@ __device__ __forceinline__ float wave_sum(float v) {
 // the last slice of the current one, so the epilogue overlaps the next tile's loads.
 // Within a round, the workgroups of one XCD (blockIdx % 8 equal) take consecutive
 // tiles, i.e. share A row panels in their L2.
-template <class T, int EPI, bool OUT3 = false>
+template <class T, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ resid, int ldr,
                                                          float* __restrict__ out, int ldo, int M,
                                                          int N, int K) {
-  static_assert(!OUT3 || (T::X6 && EPI != EPI_RESID), "P3 output: split-f32 GEMMs without residual");
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
@@ -70,43 +67,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     m0 = (t / tiles_n) * T::BM;
     n0 = (int64_t)(t % tiles_n) * T::BN;
   };
-  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
     int m0;
     int64_t n0l;
     coords(i, m0, n0l);
     const int n0 = (int)n0l;
-    if constexpr (OUT3) {
-      // out is P3 (row stride ldo floats): each 32x32 block goes through this wave's
-      // [32][36] image in the released stage, then lane (r, half) splits 16 consecutive
-      // values of row r and stores its 96-B P3 chunk (6 x 16 B, contiguous).
-      float* img = stage + wave * (32 * kLdsStride);
-      const int r = lane & 31, hf = lane >> 5;
-#pragma unroll
-      for (int tn = 0; tn < T::TN; ++tn) {
-        const int c0 = n0 + wn * T::WN + tn * 32;
-        const float b = bias[min(c0 + (lane & 31), N - 1)];
-#pragma unroll
-        for (int tm = 0; tm < T::TM; ++tm) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            float v = acc[tm][tn][e] + b;
-            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-            img[acc_row(0, e, lane) * kLdsStride + (lane & 31)] = v;
-          }
-          // one wave's LDS accesses complete in order: no barrier for its own image
-          floatx4 v4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            v4[j] = *reinterpret_cast<const floatx4*>(img + r * kLdsStride + hf * 16 + 4 * j);
-          const int row = m0 + wm * T::WM + tm * 32 + r, col = c0 + hf * 16;
-          if (row < M && col < N)
-            split_chunk_p3(v4, reinterpret_cast<uintx4*>(out + (int64_t)row * ldo + (col >> 4) * 24));
-        }
-      }
-      __syncthreads();  // the stage is refilled after the next slice
-      return;
-    }
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn) {
       const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
@@ -126,84 +91,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
         }
     }
   };
-  // P3 weights: row stride 3K/2 floats
-  const int ldw = T::P3 ? K * 3 / 2 : K;
-  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, ldw, N, K}, coords, epi);
-}
-
-// Wide split-f32 GEMM (gemm_x6w.hpp): A3 [M][K] and W3 [N][K] in P3T, one 8-wave
-// workgroup per CU walking tiles; out fp32 (row stride ldo) or, with OUT3, P3T with N
-// columns.  Same epilogues as gemm_nt_kernel.
-template <class T, int EPI, bool OUT3 = false>
-__global__ __launch_bounds__(T::THREADS, 1) void gemm_wide_kernel(const float* __restrict__ A3,
-                                                                  const float* __restrict__ W3,
-                                                                  const float* __restrict__ bias,
-                                                                  const float* __restrict__ resid,
-                                                                  int ldr, float* __restrict__ out,
-                                                                  int ldo, int M, int N, int K) {
-  static_assert(!OUT3 || EPI != EPI_RESID, "P3T output without residual");
-  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
-  const int tiles_n = (N + T::BN - 1) / T::BN;
-  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
-  const int G = gridDim.x, per_xcd = G >> 3;
-  const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
-  auto coords = [&](int i, int& m0, int& n0) {
-    const int t = i * G + xslot;
-    m0 = (t / tiles_n) * T::BM;
-    n0 = (t % tiles_n) * T::BN;
-  };
-  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float* stage) {
-    int m0, n0;
-    coords(i, m0, n0);
-    if constexpr (OUT3) {
-      float* img = stage + wave * (32 * kLdsStride);
-      const int r = lane & 31, hf = lane >> 5;
-#pragma unroll
-      for (int tn = 0; tn < T::TN; ++tn) {
-        const int c0 = n0 + wn * T::WN + tn * 32;
-        const float b = bias[min(c0 + (lane & 31), N - 1)];
-#pragma unroll
-        for (int tm = 0; tm < T::TM; ++tm) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            float v = acc[tm][tn][e] + b;
-            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-            img[acc_row(0, e, lane) * kLdsStride + (lane & 31)] = v;
-          }
-          floatx4 v4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            v4[j] = *reinterpret_cast<const floatx4*>(img + r * kLdsStride + hf * 16 + 4 * j);
-          const int row = m0 + wm * T::WM + tm * 32 + r, col = c0 + hf * 16;
-          if (row < M && col < N) p3t_store16(out, row, col, N, v4);
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int tn = 0; tn < T::TN; ++tn) {
-      const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
-      if (col >= N) continue;
-      const float b = bias[col];
-#pragma unroll
-      for (int tm = 0; tm < T::TM; ++tm)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = m0 + wm * T::WM + acc_row(tm, e, lane);
-          if (row >= M) continue;
-          float v = acc[tm][tn][e] + b;
-          if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
-          if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-          if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
-          out[(int64_t)row * ldo + col] = v;
-        }
-    }
-  };
-  walk_tiles_wide<T>(lds, n_tiles, WideOperands{A3, M, W3, N, K}, coords, epi);
+  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
 }
 
 // ---------------------------------------------------------- split-K GEMM ------
@@ -247,6 +135,22 @@ __global__ __launch_bounds__(256, 2) void gemm_splitk_kernel(const float* __rest
                 coords, epi);
 }
 
+// sum_{s<S} p[s * plane] (float4), left to right; the loads go out 8 at a time so a
+// deep split does not serialise on load latency (same additions, same order).
+__device__ __forceinline__ floatx4 sum_slabs(const float* __restrict__ p, int64_t plane, int S) {
+  floatx4 v = *reinterpret_cast<const floatx4*>(p);
+  int s = 1;
+  for (; s + 8 <= S; s += 8) {
+    floatx4 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const floatx4*>(p + (s + u) * plane);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; s < S; ++s) v += *reinterpret_cast<const floatx4*>(p + s * plane);
+  return v;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int S,
                                                             int M, int N,
@@ -258,8 +162,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   if (i4 >= (int64_t)M * n4) return;
   const int row = (int)(i4 / n4), c = (int)(i4 % n4) * 4;
   const int64_t plane = (int64_t)M * N;
-  floatx4 v = *reinterpret_cast<const floatx4*>(slab + (int64_t)row * N + c);
-  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const floatx4*>(slab + s * plane + (int64_t)row * N + c);
+  floatx4 v = sum_slabs(slab + (int64_t)row * N + c, plane, S);
   v += *reinterpret_cast<const floatx4*>(bias + c);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -271,12 +174,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 // ------------------------------------------------------- K1 / LayerNorm ------
-// One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).
 template <int VPL>
 __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __restrict__ g,
                                              const float* __restrict__ b, float eps,
-                                             float* __restrict__ dst, float* __restrict__ dst3,
-                                             int64_t row, int lane) {
+                                             float* __restrict__ dst, int lane) {
   constexpr int H = VPL * 256;
   float s = 0.f;
 #pragma unroll
@@ -294,17 +195,43 @@ __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __r
     const int c = (i * 64 + lane) * 4;
     const floatx4 gg = *reinterpret_cast<const floatx4*>(g + c);
     const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c);
-    const floatx4 y = x[i] * rstd * gg + bb;
-    *reinterpret_cast<floatx4*>(dst + c) = y;
-    if (dst3) p3t_store4(dst3, row, c, H, y);  // P3T copy for a split-f32 consumer
+    *reinterpret_cast<floatx4*>(dst + c) = x[i] * rstd * gg + bb;
   }
 }
 
+// Split-K reduction of a residual projection fused with the LayerNorm after it (few-row
+// path: saves a launch and the y round trip per LN): x = LN(sum_s slab[s] + bias +
+// resid), one wave per row, slabs summed in order - bit-identical to
+// splitk_reduce_kernel<EPI_RESID> followed by ln_kernel.  A wave reads its whole row
+// before writing it, so dst may alias resid row for row (stride H).
+template <int VPL>
+__global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(
+    const float* __restrict__ slab, int S, int M, const float* __restrict__ bias,
+    const float* resid, int ldr, const float* __restrict__ g, const float* __restrict__ b,
+    float eps, float* dst) {
+  constexpr int H = VPL * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int64_t plane = (int64_t)M * H;
+  floatx4 x[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    floatx4 v = sum_slabs(slab + (int64_t)row * H + c, plane, S);
+    v += *reinterpret_cast<const floatx4*>(bias + c);
+    v += *reinterpret_cast<const floatx4*>(resid + (int64_t)row * ldr + c);
+    x[i] = v;
+  }
+  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, lane);
+}
+
+// One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).
 template <int VPL>
 __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int* __restrict__ ids, int M, int L, int vocab, const float* __restrict__ word,
     const float* __restrict__ pos, const float* __restrict__ typ, const float* __restrict__ g,
-    const float* __restrict__ b, float eps, float* __restrict__ out, float* __restrict__ out3) {
+    const float* __restrict__ b, float eps, float* __restrict__ out) {
   constexpr int H = VPL * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -320,14 +247,14 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
            *reinterpret_cast<const floatx4*>(pos + (int64_t)p * H + c) +
            *reinterpret_cast<const floatx4*>(typ + c);
   }
-  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, out3, row, lane);
+  ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, lane);
 }
 
 template <int VPL>
 __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, int M,
                                                  const float* __restrict__ g,
                                                  const float* __restrict__ b, float eps,
-                                                 float* __restrict__ dst, float* __restrict__ dst3) {
+                                                 float* __restrict__ dst) {
   constexpr int H = VPL * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -336,7 +263,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 #pragma unroll
   for (int i = 0; i < VPL; ++i)
     x[i] = *reinterpret_cast<const floatx4*>(src + (int64_t)row * H + (i * 64 + lane) * 4);
-  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, dst3, row, lane);
+  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, lane);
 }
 
 // ------------------------------------------------------------ K3 attention ----
@@ -353,8 +280,7 @@ constexpr int kDh = 64;
 __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
                                                        const int* __restrict__ mask, int L,
                                                        int H, int heads, int q_tiles,
-                                                       float scale, float* __restrict__ ctx,
-                                                       float* __restrict__ ctx3, int cls_compact) {
+                                                       float scale, float* __restrict__ ctx) {
   __shared__ float obuf[32][kDh + 1];
   const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
   const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
@@ -443,18 +369,6 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
   }
   __syncthreads();
   const int nrows = min(32, L - q0);
-  if (ctx3) {  // P3T for a split-f32 consumer: lane takes (query, 16-dim chunk) items;
-               // cls_compact: only the CLS row, stored as row bseq
-    const int nq = cls_compact ? 1 : nrows;
-    for (int it = lane; it < nq * (kDh / 16); it += 64) {
-      const int q = it >> 2, ch = it & 3;
-      floatx4 v4[4];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v4[j >> 2][j & 3] = obuf[q][ch * 16 + j];
-      p3t_store16(ctx3, cls_compact ? bseq : row0 + q0 + q, h * kDh + ch * 16, H, v4);
-    }
-    return;
-  }
   for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
 }
 
@@ -526,8 +440,6 @@ struct Buf {
 
 struct LayerW {
   const float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
-  // P3T copies of the four projection matrices (split-f32 path), in mq_encoder::wp3
-  const float *wqkv3 = nullptr, *wo3 = nullptr, *w13 = nullptr, *w23 = nullptr;
 };
 
 int64_t weight_count(const mq_bert_config& c) {
@@ -555,12 +467,12 @@ struct GemmArgs {
   int M, N, K;
 };
 
-template <class T, int EPI, bool OUT3 = false>
+template <class T, int EPI>
 void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s) {
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
   // persistent grid: at most two workgroups per CU, rounded up to a multiple of 8
   const int grid = (std::min(tiles, 2 * num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, OUT3>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
                      g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
 }
 
@@ -568,34 +480,20 @@ using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128
 using GemmT96 = F32Tile<4, 1, 1, 3>;    // 128 x 96
 using GemmMid = F32Tile<2, 2, 2, 1>;    // 128 x 64
 using GemmSmall = F32Tile<1, 4, 1, 1>;  // 32 x 128  (few rows)
-using X6Big = F32Tile<2, 2, 2, 2, true>;  // 128 x 128, split-f32, fp32 operands split in-kernel
+
+// Pick the tile whose launch wastes the least: every CU runs two workgroups at a time,
+// so a grid that is not a multiple of 2*CUs idles part of the chip in its last round
+// (M = 8192: N = 768 -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost model:
+// rounds * tile area / relative tile efficiency.
+using X6Big = F32Tile<2, 2, 2, 2, true>;  // 128 x 128, split-f32
 using X6T96 = F32Tile<4, 1, 1, 3, true>;  // 128 x 96
 using X6Mid = F32Tile<2, 2, 2, 1, true>;  // 128 x 64
-using P3Big = F32Tile<2, 2, 2, 2, true, 2, false, true>;  // 128 x 128, split-f32, P3 operands
-using P3T96 = F32Tile<4, 1, 1, 3, true, 2, false, true>;  // 128 x 96
-using P3Mid = F32Tile<2, 2, 2, 1, true, 2, false, true>;  // 128 x 64
 
-using WideA = WTile<8, 1, 1, 3, 2>;  // 256 x 96, 8 waves of 32 x 96, 32-deep stages
-using WideB = WTile<4, 2, 2, 2, 2>;  // 256 x 128, 8 waves of 64 x 64
-
-template <class T, int EPI, bool OUT3 = false>
-void launch_wide_t(const GemmArgs& g, int num_cus, hipStream_t s) {
-  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-  // persistent grid: one 8-wave workgroup per CU, a multiple of 8 (XCD remap)
-  const int grid = (std::min(tiles, num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_wide_kernel<T, EPI, OUT3>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.W,
-                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
-}
-
-// Tile codes (also the mq_debug_gemm_f32 `tile` argument):
-//   0-3 exact f32 128x128 / 128x96 / 128x64 / 32x128, 4 split-K (host path only),
-//   5-7 split-f32 with the split in the staging (fp32 operands), same three geometries,
-//   8-10 split-f32 on P3 operands (A and W pre-split), 11-13 the same with a P3 output,
-//   14 / 15 the wide 8-wave split-f32 kernel 256x96 / 256x128 on P3T operands, 16 / 17
-//   the same writing P3T.
+// Tile codes (also the mq_debug_gemm_f32 `tile` argument): 0-3 exact f32 128x128 /
+// 128x96 / 128x64 / 32x128, 4 split-K (host path only), 5-7 split-f32 128x128 / 128x96
+// / 128x64.
 template <int EPI>
 void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
-  constexpr bool kP3Out = EPI != EPI_RESID;
   switch (tile) {
     case 0: launch_gemm_t<GemmBig, EPI>(g, num_cus, s); return;
     case 1: launch_gemm_t<GemmT96, EPI>(g, num_cus, s); return;
@@ -603,16 +501,6 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
     case 5: launch_gemm_t<X6Big, EPI>(g, num_cus, s); return;
     case 6: launch_gemm_t<X6T96, EPI>(g, num_cus, s); return;
     case 7: launch_gemm_t<X6Mid, EPI>(g, num_cus, s); return;
-    case 8: launch_gemm_t<P3Big, EPI>(g, num_cus, s); return;
-    case 9: launch_gemm_t<P3T96, EPI>(g, num_cus, s); return;
-    case 10: launch_gemm_t<P3Mid, EPI>(g, num_cus, s); return;
-    case 11: if constexpr (kP3Out) launch_gemm_t<P3Big, EPI, kP3Out>(g, num_cus, s); return;
-    case 12: if constexpr (kP3Out) launch_gemm_t<P3T96, EPI, kP3Out>(g, num_cus, s); return;
-    case 13: if constexpr (kP3Out) launch_gemm_t<P3Mid, EPI, kP3Out>(g, num_cus, s); return;
-    case 14: launch_wide_t<WideA, EPI>(g, num_cus, s); return;
-    case 15: launch_wide_t<WideB, EPI>(g, num_cus, s); return;
-    case 16: if constexpr (kP3Out) launch_wide_t<WideA, EPI, kP3Out>(g, num_cus, s); return;
-    case 17: if constexpr (kP3Out) launch_wide_t<WideB, EPI, kP3Out>(g, num_cus, s); return;
     default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); return;
   }
 }
@@ -625,8 +513,15 @@ int splitk_factor(const GemmArgs& g, int num_cus) {
   const int64_t slots = 2 * (int64_t)num_cus;
   if (tiles * 2 > slots || g.M > 256) return 0;
   const int slices = g.K / kBK;
+  // At most 16 chunks: deeper splits fill more CUs but the slab traffic and the ordered
+  // reduction grow with S (single query, L=32: encoder p50 0.74 ms at 16 vs 0.88 ms at
+  // 64, 0.80 ms at 8).  MQ_SPLITK_MAX overrides it for tuning.
+  static const int cap = [] {
+    const char* v = getenv("MQ_SPLITK_MAX");
+    return v && atoi(v) >= 2 ? atoi(v) : 16;
+  }();
   int best = 1;
-  for (int s = 1; s <= slices; ++s)
+  for (int s = 1; s <= slices && s <= cap; ++s)
     if (slices % s == 0 && tiles * s <= slots && (size_t)s * g.M * g.N <= g.slab_floats) best = s;
   return best >= 2 ? best : 0;
 }
@@ -642,10 +537,30 @@ void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
                      s, g.slab, S, g.M, g.N, g.bias, g.resid, g.ldr, g.out, g.ldo);
 }
 
-// Geometry with the least waste: every CU runs two workgroups at a time, so a grid that
-// is not a multiple of 2*CUs idles part of the chip in its last round (M = 8192: N = 768
-// -> 128x96 gives exactly 512 tiles; 2304 -> 1536).  Cost: rounds * area / efficiency.
-int pick_tile(const GemmArgs& g, int num_cus, bool x6) {
+template <int EPI>
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false) {
+  const int S = splitk_factor(g, num_cus);
+  if (S) {
+    launch_splitk<EPI>(g, S, s);
+    return;
+  }
+  if (x6) {  // split-f32 tiles: same waste model over 128x{128,96,64}
+    const int bns[3] = {128, 96, 64};
+    const double effs[3] = {1.0, 0.96, 0.9};
+    const int64_t slots = 2 * (int64_t)num_cus;
+    int best = 0;
+    double best_cost = 1e300;
+    for (int i = 0; i < 3; ++i) {
+      const int64_t tiles = (int64_t)((g.M + 127) / 128) * ((g.N + bns[i] - 1) / bns[i]);
+      const double cost = (double)((tiles + slots - 1) / slots) * 128 * bns[i] / effs[i];
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = i;
+      }
+    }
+    launch_gemm_tile<EPI>(g, 5 + best, num_cus, s);
+    return;
+  }
   struct Cand {
     int bm, bn;
     double eff;
@@ -654,7 +569,7 @@ int pick_tile(const GemmArgs& g, int num_cus, bool x6) {
   const int64_t slots = 2 * (int64_t)num_cus;
   int best = 0;
   double best_cost = 1e300;
-  for (int i = 0; i < (x6 ? 3 : 4); ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int64_t tiles = (int64_t)((g.M + cands[i].bm - 1) / cands[i].bm) * ((g.N + cands[i].bn - 1) / cands[i].bn);
     const int64_t rounds = (tiles + slots - 1) / slots;
     const double cost = (double)rounds * cands[i].bm * cands[i].bn / cands[i].eff;
@@ -663,33 +578,7 @@ int pick_tile(const GemmArgs& g, int num_cus, bool x6) {
       best = i;
     }
   }
-  return best;
-}
-
-// Does this GEMM run on the split-f32 P3 path?  (Not when it is split-K: that path is
-// exact f32 on fp32 operands.)
-bool gemm_uses_p3(const GemmArgs& g, int num_cus, int precision) {
-  return precision == MQ_DTYPE_F32X6 && splitk_factor(g, num_cus) == 0;
-}
-
-// out = epi(A W^T + b (+ resid)).  p3 = the split-f32 path: A and W are P3T, and with
-// out3 the output is written as P3T (not with a residual).
-template <int EPI>
-void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool p3 = false, bool out3 = false) {
-  const int S = splitk_factor(g, num_cus);
-  if (S) {
-    launch_splitk<EPI>(g, S, s);
-    return;
-  }
-  if (p3) {  // wide split-f32 kernel on P3T operands: 256x96 or 256x128, one WG per CU
-    const int64_t mt = (g.M + 255) / 256;
-    const int64_t ra = (mt * ((g.N + 95) / 96) + num_cus - 1) / num_cus;
-    const int64_t rb = (mt * ((g.N + 127) / 128) + num_cus - 1) / num_cus;
-    const bool wide_b = rb * 128 < ra * 96;
-    launch_gemm_tile<EPI>(g, (out3 ? 16 : 14) + (wide_b ? 1 : 0), num_cus, s);
-    return;
-  }
-  launch_gemm_tile<EPI>(g, pick_tile(g, num_cus, false), num_cus, s);
+  launch_gemm_tile<EPI>(g, best, num_cus, s);
 }
 
 // Stage labels for the optional per-kernel-class event timeline.
@@ -707,9 +596,6 @@ struct mq_encoder {
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
   Buf x, y, qkv, ctx, ffn, io_out, slab;
-  // split-f32 path: P3T weights (converted once per load) and P3T activations
-  Buf wp3, xp, ctxp, ffnp;
-  bool wp3_ready = false;
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -733,37 +619,35 @@ struct mq_encoder {
 namespace {
 
 template <int EPI>
-void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s, bool p3 = false,
-          bool out3 = false) {
+void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s, p3, out3);
+  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6);
 }
 
-// Split the four projection matrices of every layer into P3T (once per weight load).
-int ensure_p3_weights(mq_encoder* e, hipStream_t s) {
-  if (e->wp3_ready) return MQ_OK;
-  const int64_t H = e->cfg.hidden, F = e->cfg.ffn;
-  const int64_t per_layer = p3t_floats(3 * H, (int)H) + p3t_floats(H, (int)H) + p3t_floats(F, (int)H) +
-                            p3t_floats(H, (int)F);
-  int rc = e->wp3.ensure((size_t)(per_layer * e->layers.size()));
-  if (rc) return rc;
-  float* p = e->wp3.p;
-  for (LayerW& w : e->layers) {
-    auto split = [&](const float* src, int64_t rows, int64_t k) {
-      launch_split_p3t(src, k, rows, (int)k, p, s);
-      const float* r = p;
-      p += p3t_floats(rows, (int)k);
-      return r;
-    };
-    w.wqkv3 = split(w.wqkv, 3 * H, H);
-    w.wo3 = split(w.wo, H, H);
-    w.w13 = split(w.w1, F, H);
-    w.w23 = split(w.w2, H, F);
+// Residual projection + LayerNorm: x = LN(A W^T + b + resid), through y (g.out) on the
+// tiled path; on the split-K (few-row) path the slab reduction, residual and LN run as
+// one kernel writing x directly (bit-identical).  The fused form needs resid rows at
+// stride H (a wave overwrites only the row it has read).
+template <int VPL>
+void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const float* lnb, float* x,
+                   int stage, hipStream_t s) {
+  const int H = VPL * 256;
+  const unsigned rb = (unsigned)((g.M + 3) / 4);
+  const int S = splitk_factor(g, e->num_cus);
+  if (S && g.ldr == H && g.N == H) {
+    using T = F32Tile<1, 4, 1, 1>;
+    e->tl.mark(s, stage);
+    const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+    hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W, g.M,
+                       g.N, g.K, S, g.slab);
+    e->tl.mark(s, ST_LN);
+    hipLaunchKernelGGL((splitk_reduce_ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, g.slab, S, g.M, g.bias,
+                       g.resid, g.ldr, lng, lnb, e->cfg.ln_eps, x);
+    return;
   }
-  MQ_HIP(hipGetLastError());
-  MQ_HIP(hipStreamSynchronize(s));
-  e->wp3_ready = true;
-  return MQ_OK;
+  gemm<EPI_RESID>(e, g, stage, s);
+  e->tl.mark(s, ST_LN);
+  hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, g.out, g.M, lng, lnb, e->cfg.ln_eps, x);
 }
 
 // One forward.  With CLS pooling the last layer only needs the CLS rows after its
@@ -778,67 +662,31 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
   const unsigned row_blocks = (unsigned)((M + 3) / 4);
   const float scale = 1.0f / sqrtf((float)(H / c.heads));
   const int q_tiles = (L + 31) / 32;
-  // which GEMMs run split-f32 on P3 operands; their producers then write P3 copies
-  auto p3 = [&](int m, int n, int k) {
-    const GemmArgs g{e->slab.p, e->slab.n, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, m, n, k};
-    return gemm_uses_p3(g, e->num_cus, e->precision);
-  };
-  bool qkv_p3 = p3(M, 3 * H, H);
   e->tl.mark(s, ST_EMBED);
   hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, ids, M, L,
-                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p,
-                     qkv_p3 ? e->xp.p : nullptr);
+                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p);
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
     const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
     // rows this layer carries past attention: all M tokens, or the B CLS rows
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
-    const unsigned rb = (unsigned)((rows + 3) / 4);
-    const bool o_p3 = p3(rows, H, H), up_p3 = p3(rows, F, H), down_p3 = p3(rows, H, F);
-    const bool next_qkv_p3 = li + 1 < e->layers.size() && p3(M, 3 * H, H);
-    if (qkv_p3)
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->xp.p, 0, w.wqkv3, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
-                     ST_QKV, s, true);
-    else
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
-                     ST_QKV, s);
+    gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+                   ST_QKV, s);
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p, o_p3 ? e->ctxp.p : nullptr, cls_only ? 1 : 0);
-    // y = x + ctx Wo^T + bo  (compact [rows, H])
-    if (o_p3)
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctxp.p, 0, w.wo3, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
-                      ST_OPROJ, s, true);
-    else
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
-                      ST_OPROJ, s);
-    e->tl.mark(s, ST_LN);
-    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln1g, w.ln1b,
-                       c.ln_eps, e->x.p, up_p3 ? e->xp.p : nullptr);
-    // FFN up: GELU output straight to P3 when both FFN GEMMs run split-f32
-    const bool ffn3 = up_p3 && down_p3;
-    const GemmArgs up = up_p3
-        ? GemmArgs{e->slab.p, e->slab.n, e->xp.p, 0, w.w13, w.b1, nullptr, 0, ffn3 ? e->ffnp.p : e->ffn.p,
-                   F, rows, F, H}
-        : GemmArgs{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
+                       H, c.heads, qt, scale, e->ctx.p);
+    // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y)
+    gemm_resid_ln<VPL>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
+                       w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
+    const GemmArgs up{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
     if (c.gelu == MQ_GELU_TANH)
-      gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s, up_p3, ffn3);
+      gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s);
     else
-      gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s, up_p3, ffn3);
-    if (down_p3) {
-      if (!ffn3) launch_split_p3t(e->ffn.p, F, rows, F, e->ffnp.p, s);
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffnp.p, 0, w.w23, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
-                      ST_FFN_DOWN, s, true);
-    } else {
-      gemm<EPI_RESID>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
-                      ST_FFN_DOWN, s);
-    }
-    e->tl.mark(s, ST_LN);
-    hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, e->y.p, rows, w.ln2g, w.ln2b,
-                       c.ln_eps, e->x.p, next_qkv_p3 ? e->xp.p : nullptr);
-    qkv_p3 = next_qkv_p3;
+      gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
+    gemm_resid_ln<VPL>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
+                       w.ln2g, w.ln2b, e->x.p, ST_FFN_DOWN, s);
   }
   e->tl.mark(s, ST_POOL);
   const bool pruned = c.pooling == MQ_POOL_CLS;  // x holds [B, H] CLS rows
@@ -868,10 +716,9 @@ constexpr size_t kMaxGraphs = 6;
 // Replay the forward io_ids/io_mask -> io_out for (B, L) as one hipGraph launch on s,
 // capturing it first if no cached graph matches the shape, precision and buffers.
 int launch_graph(mq_encoder* e, int B, int L, hipStream_t s) {
-  const std::vector<const void*> bufs = {e->weights.p, e->x.p,    e->y.p,      e->qkv.p,
-                                         e->ctx.p,     e->ffn.p,  e->slab.p,   e->io_out.p,
-                                         e->io_ids,    e->io_mask, e->wp3.p,    e->xp.p,
-                                         e->ctxp.p,    e->ffnp.p};
+  const std::vector<const void*> bufs = {e->weights.p, e->x.p,   e->y.p,      e->qkv.p,
+                                         e->ctx.p,     e->ffn.p, e->slab.p,   e->io_out.p,
+                                         e->io_ids,    e->io_mask};
   mq_encoder::Graph* hit = nullptr;
   for (auto& g : e->graphs)
     if (g.B == B && g.L == L && g.precision == e->precision && g.bufs == bufs) hit = &g;
@@ -958,8 +805,7 @@ int mq_encoder_destroy(mq_encoder* e) {
   if (!e) return MQ_OK;
   {
     DeviceGuard dg(e->device);
-    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab,
-                   &e->wp3, &e->xp, &e->ctxp, &e->ffnp})
+    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab})
       b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
@@ -1012,7 +858,6 @@ int mq_encoder_load_weights(mq_encoder* e, const float* blob, int64_t n_floats) 
     e->layers.push_back(w);
   }
   e->loaded = true;
-  e->wp3_ready = false;  // P3 weights are re-split at the next split-f32 forward
   return MQ_OK;
 }
 
@@ -1031,18 +876,12 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 17, "bad epi/tile");
-  MQ_CHECK_ARG(!((tile >= 11 && tile <= 13) || tile >= 16) || (epi != EPI_RESID && N % 16 == 0),
-               "P3 output: no residual, N %% 16 == 0");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 7, "bad epi/tile");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   GemmArgs g{nullptr, 0, A, K, W, bias, resid, N, out, N, M, N, K};
   hipStream_t s = (hipStream_t)stream;
-  if (tile >= 8 && tile <= 13) {  // A and W are P3 (mq_debug_split_p3); 11-13 write P3
-    g.lda = K * 3 / 2;
-    if (tile >= 11) g.ldo = N * 3 / 2;
-  }  // 14-17: A and W are P3T (mq_debug_split_p3t); 16-17 write `out` as P3T
   if (tile == 4) {  // split-K path (test hook: allocates its own slab)
     MQ_CHECK_ARG(N % 4 == 0, "split-K needs N %% 4 == 0");
     const int slices = K / kBK;
@@ -1071,22 +910,6 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
     case EPI_GELU_TANH: launch_gemm_tile<EPI_GELU_TANH>(g, tile, cus, s); break;
     default: launch_gemm_tile<EPI_RESID>(g, tile, cus, s); break;
   }
-  MQ_HIP(hipGetLastError());
-  return MQ_OK;
-}
-
-int mq_debug_split_p3t(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream) {
-  clear_error();
-  MQ_CHECK_ARG(src && dst && rows >= 0 && K > 0 && K % 16 == 0 && lds >= K, "bad split_p3t arguments");
-  launch_split_p3t(src, lds, rows, K, dst, (hipStream_t)stream);
-  MQ_HIP(hipGetLastError());
-  return MQ_OK;
-}
-
-int mq_debug_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst, void* stream) {
-  clear_error();
-  MQ_CHECK_ARG(src && dst && rows >= 0 && K > 0 && K % 16 == 0 && lds >= K, "bad split_p3 arguments");
-  launch_split_p3(src, lds, rows, K, dst, (hipStream_t)stream);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1142,16 +965,6 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
                   std::make_pair(&e->ffn, M * c.ffn)}) {
     rc = bn.first->ensure(bn.second);
-    if (rc) return rc;
-  }
-  if (e->precision == MQ_DTYPE_F32X6) {  // P3 activations + weights of the split-f32 path
-    for (auto bn : {std::make_pair(&e->xp, (size_t)p3t_floats(M, c.hidden)),
-                    std::make_pair(&e->ctxp, (size_t)p3t_floats(M, c.hidden)),
-                    std::make_pair(&e->ffnp, (size_t)p3t_floats(M, c.ffn))}) {
-      rc = bn.first->ensure(bn.second);
-      if (rc) return rc;
-    }
-    rc = ensure_p3_weights(e, s);
     if (rc) return rc;
   }
   const bool graph = e->use_graphs && !e->tl.on;

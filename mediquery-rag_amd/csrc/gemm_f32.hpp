@@ -35,7 +35,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
 template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2,
-          bool BF16_ = false, bool P3_ = false>
+          bool BF16_ = false>
 struct F32Tile {
   static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
   static constexpr bool X6 = X6_;
@@ -45,17 +45,12 @@ struct F32Tile {
   // a 32-slot slice carries 64 k-values; only the MFMA (32x32x16 bf16) differs.
   static constexpr bool BF16 = BF16_;
   static_assert(!(X6 && BF16), "one arithmetic mode");
-  // P3: both operands arrive PRE-SPLIT in the planar layout of split_p3 (below): row r,
-  // k-chunk c holds [3 planes][16] bf16 = 96 B at byte r * 6K + c * 96, i.e. exactly the
-  // staged LDS row image of the X6 path - staging is a plain 16-B copy, no VALU split.
-  static constexpr bool P3 = P3_;
-  static_assert(!P3 || X6, "pre-split operands feed the split-f32 MFMA path");
   static constexpr int WM = TM * 32, WN = TN * 32;  // wave tile
   static constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   static constexpr int THREADS = WAVES_M * WAVES_N * kWave;
   static constexpr int ROWS = BM + BN;
   static constexpr int BK = X6 ? 16 : 32;                 // K per staged slice
-  static constexpr int F4_PER_ROW = P3 ? 6 : BK / 4;      // 16-B pieces per row per slice
+  static constexpr int F4_PER_ROW = BK / 4;               // float4 per row per slice
   static constexpr int ROW_FLOATS = X6 ? 28 : kLdsStride; // LDS row stride in 4-B words
   static constexpr int TOTAL_F4 = ROWS * F4_PER_ROW;                  // float4 per slice
   static constexpr int LOADS = (TOTAL_F4 + THREADS - 1) / THREADS;      // per thread
@@ -89,44 +84,6 @@ __device__ __forceinline__ void split3(floatx4 x, uint2 (&pl)[3]) {
   }
 }
 
-// ---- P3: the planar pre-split layout -------------------------------------------
-// A [R][K] fp32 matrix (K % 16 == 0) as [R][K/16][3][16] bf16: 6K bytes per row, chunk c
-// of row r at byte r*6K + c*96, plane p of the chunk at +32p.  The planes are split3's
-// (round-to-nearest at each step), so a P3 operand stages to the same LDS bytes as the
-// in-kernel split and every X6 GEMM result is bit-identical either way.  As a float*
-// operand a P3 matrix has a row stride of 3K/2 floats.
-__device__ __forceinline__ void split_chunk_p3(const floatx4 (&v)[4], uintx4* __restrict__ dst) {
-  uint2 pl[4][3];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) split3(v[c], pl[c]);
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    dst[2 * p] = uintx4{pl[0][p].x, pl[0][p].y, pl[1][p].x, pl[1][p].y};
-    dst[2 * p + 1] = uintx4{pl[2][p].x, pl[2][p].y, pl[3][p].x, pl[3][p].y};
-  }
-}
-
-// src [rows][K] fp32 (row stride lds floats) -> dst P3; one thread per 16-float chunk.
-template <int Unused = 0>
-__global__ __launch_bounds__(256) void split_p3_kernel(const float* __restrict__ src, int64_t lds,
-                                                       int64_t rows, int K, float* __restrict__ dst) {
-  const int64_t chunks = K >> 4;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= rows * chunks) return;
-  const int64_t r = i / chunks, c = i - r * chunks;
-  const floatx4* s = reinterpret_cast<const floatx4*>(src + r * lds + c * 16);
-  const floatx4 v[4] = {s[0], s[1], s[2], s[3]};
-  split_chunk_p3(v, reinterpret_cast<uintx4*>(dst + r * ((int64_t)K * 3 / 2) + c * 24));
-}
-
-inline void launch_split_p3(const float* src, int64_t lds, int64_t rows, int K, float* dst,
-                            hipStream_t s) {
-  const int64_t n = rows * (K >> 4);
-  if (n > 0)
-    hipLaunchKernelGGL(split_p3_kernel<0>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src,
-                       lds, rows, K, dst);
-}
-
 // One K-slice of both operands, held in registers between the global load and the
 // LDS write (T14 "issue early / write late").  Rows past M / N are clamped onto the
 // last valid row instead of being zeroed: an MFMA output element depends only on its
@@ -150,8 +107,7 @@ struct Stager {
       } else {
         p = B + min(n0 + (int64_t)(row - T::BM), N - 1) * ldb;
       }
-      // P3 rows: chunk k0/16 of 96 B = 24 floats; fp32 rows: k0 floats
-      r[i] = *reinterpret_cast<const floatx4*>(p + (T::P3 ? (k0 >> 4) * 24 : k0) + ch * 4);
+      r[i] = *reinterpret_cast<const floatx4*>(p + k0 + ch * 4);
     }
   }
 
@@ -161,7 +117,7 @@ struct Stager {
       const int f = tid + i * T::THREADS;
       if (T::PARTIAL && i == T::LOADS - 1 && f >= T::TOTAL_F4) break;
       const int row = f / T::F4_PER_ROW, ch = f % T::F4_PER_ROW;
-      if constexpr (T::X6 && !T::P3) {
+      if constexpr (T::X6) {
         uint2 pl[3];
         split3(r[i], pl);
         char* base = reinterpret_cast<char*>(stage + row * T::ROW_FLOATS) + ch * 8;

@@ -42,6 +42,19 @@ __global__ __launch_bounds__(256) void add_rows_kernel(const float* __restrict__
   }
 }
 
+// Row gather for select/compaction: one wave per output row, a plain copy (stored rows
+// are already unit-norm, so no re-normalisation).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ src,
+                                                          const int64_t* __restrict__ sel, int64_t n,
+                                                          int dim, float* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const floatx4* s = reinterpret_cast<const floatx4*>(src + sel[r] * dim);
+  floatx4* d = reinterpret_cast<floatx4*>(dst + r * dim);
+  for (int i = lane; i < (dim >> 2); i += 64) d[i] = s[i];
+}
+
 // ================================================ K9: fused score + top-k ======
 // Register-resident running top-KC list per lane, kept sorted by (score desc, id asc).
 template <int KC>
@@ -84,7 +97,7 @@ struct TopList {
 
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
-using SearchWideX6 = F32Tile<2, 2, 2, 2, true, 2, false, true>;  // split-f32 on P3 operands
+using SearchWideX6 = F32Tile<2, 2, 2, 2, true>;  // same, split-f32 arithmetic
 using SearchWideBF = F32Tile<2, 2, 2, 2, false, 2, true>;    // bf16 coarse scan
 using SearchNarrowBF = F32Tile<1, 4, 1, 1, false, 2, true>;  // bf16 coarse, small batches
 using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
@@ -168,8 +181,7 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
       __syncthreads();
     }
   };
-  const int ld = T::P3 ? dim * 3 / 2 : dim;  // P3 rows: 3*dim/2 floats
-  walk_tiles<T>(lds, n_tiles, TileOperands{Q, ld, nq, C, ld, n_rows, dim}, coords, epi);
+  walk_tiles<T>(lds, n_tiles, TileOperands{Q, dim, nq, C, dim, n_rows, dim}, coords, epi);
 
   const int list = (g * T::WAVES_N + wn) * S::LPQ + part;
   const int qg = m0 + wm * T::WM + q_local;
@@ -190,7 +202,8 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
 // streaming dot-product kernel instead: 16 lanes per row (each 16-B load instruction
 // of a wave covers four 256-B row segments), queries in LDS, two rows in flight per
 // lane group, fp32 FMA, a 16-lane butterfly per (row, query), and lane j of the group
-// keeps query j's register top list.  List = lane group: cand[group][query][0..kl).
+// keeps query j's register top list; the block merges its 16 groups' lists at the end.
+// List = block: cand[block][query][0..kl).
 constexpr int kStreamMaxNV = 16;  // float4 per lane per row: dim <= 1024
 
 template <int NQ, int KC, int NV>
@@ -256,14 +269,54 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
     }
     score_rows(v, r0, nr);
   }
+  // Block-level merge of the 16 lane groups' lists: one list per (block, query), so K10
+  // merges 16x fewer lists (for a single query its 8192-list merge was 78 us).  Lists go
+  // through LDS (the query image is dead by now); wave j % 4 merges query j: lane l folds
+  // candidates l, l+64, ... into a register list, then kl wave arg-best rounds emit the
+  // block's sorted list.  The K10 overflow check stays sound: a group list that dropped
+  // a top-k member holds kl entries better than the k-th result, so the block list does.
+  __syncthreads();
+  float* lst_s = qs;                                       // [16][NQ][KC]
+  int* lst_i = reinterpret_cast<int*>(qs + 16 * NQ * KC);  // [16][NQ][KC]
   if (owner) {
-    const int64_t base = (group * nq + gl) * kl;
+    const int g = tid >> 4;
 #pragma unroll
-    for (int i = 0; i < KC; ++i)
-      if (i < kl) {
-        cand_s[base + i] = top.s[i];
-        cand_i[base + i] = top.id[i];
+    for (int i = 0; i < KC; ++i) {
+      lst_s[(g * NQ + gl) * KC + i] = top.s[i];
+      lst_i[(g * NQ + gl) * KC + i] = top.id[i];
+    }
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int j = wave; j < min(nq, NQ); j += 4) {
+    TopList<KC> t;
+    t.init();
+    for (int c = lane; c < 16 * kl; c += 64) {
+      const int g = c / kl, i = c - g * kl;
+      const float x = lst_s[(g * NQ + j) * KC + i];
+      const int xi = lst_i[(g * NQ + j) * KC + i];
+      if (xi >= 0 && t.beats_tail(x, xi)) t.insert(x, xi);
+    }
+    const int64_t base = ((int64_t)blockIdx.x * nq + j) * kl;
+    for (int r = 0; r < kl; ++r) {
+      float bs = t.s[0];
+      int bi = t.id[0], bt = lane;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const float os = __shfl_xor(bs, off);
+        const int oi = __shfl_xor(bi, off), ot = __shfl_xor(bt, off);
+        if (better(os, oi, bs, bi)) {
+          bs = os;
+          bi = oi;
+          bt = ot;
+        }
       }
+      if (lane == 0) {
+        cand_s[base + r] = bs;
+        cand_i[base + r] = bi;
+      }
+      if (lane == bt && bi >= 0) t.pop_front();
+    }
   }
 }
 
@@ -526,9 +579,6 @@ struct mq_index {
   DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
   int64_t n16 = 0;   // rows already mirrored into rows16
   DevBuf q16, coarse_s, coarse_i;
-  DevBuf rows3;      // P3 shadow of `rows` for the split-f32 scan ([cap, 3*dim/2] floats)
-  int64_t n3 = 0;    // rows already mirrored into rows3
-  DevBuf q3;         // P3 copy of the query batch
   DevBuf flag;          // merge overflow flag (k > 16)
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
   int64_t remerges = 0;  // merges re-run with 64-entry thread lists
@@ -543,9 +593,8 @@ namespace {
 template <class T, int KC>
 void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int nqt,
                    float* cs, int* ci, hipStream_t s) {
-  // bf16 tiles read the bf16 shadow as float-typed rows of half the width; split-f32
-  // tiles the P3 shadow (and P3 queries)
-  const float* rows = T::BF16 ? ix->rows16.as<float>() : (T::P3 ? ix->rows3.as<float>() : ix->rows);
+  // bf16 tiles read the bf16 shadow as float-typed rows of half the width
+  const float* rows = T::BF16 ? ix->rows16.as<float>() : ix->rows;
   const int dim = T::BF16 ? ix->dim / 2 : ix->dim;
   hipLaunchKernelGGL((flat_search_kernel<T, KC>), dim3(G * nqt), dim3(256), 0, s, q, nq, rows,
                      ix->n, dim, G, nqt, k, cs, ci);
@@ -609,13 +658,19 @@ enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16, SCAN_STREAM };
 template <int NQ, int KC>
 void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
                       int* ci, hipStream_t s) {
-  const size_t lds = (size_t)NQ * ix->dim * sizeof(float);
+  // query image, then the block merge's [16][NQ][KC] (score, id) lists in the same LDS
+  const size_t lds = std::max((size_t)NQ * ix->dim * sizeof(float), (size_t)16 * NQ * KC * 8);
+  auto launch = [&](auto kern) {
+    if (lds > 64 * 1024)  // above the default dynamic-LDS limit (64-entry lists, NQ >= 8)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, q, nq, ix->rows, ix->n, ix->dim, kl, cs,
+                       ci);
+  };
   if (ix->dim == 768)  // the dmeta / BERT-base width, register arrays sized exactly
-    hipLaunchKernelGGL((stream_search_kernel<NQ, KC, 12>), dim3(blocks), dim3(256), lds, s, q, nq,
-                       ix->rows, ix->n, ix->dim, kl, cs, ci);
+    launch(stream_search_kernel<NQ, KC, 12>);
   else
-    hipLaunchKernelGGL((stream_search_kernel<NQ, KC, kStreamMaxNV>), dim3(blocks), dim3(256), lds,
-                       s, q, nq, ix->rows, ix->n, ix->dim, kl, cs, ci);
+    launch(stream_search_kernel<NQ, KC, kStreamMaxNV>);
 }
 
 template <int KC>
@@ -639,8 +694,8 @@ int stream_blocks(const mq_index* ix) {
 }
 
 template <int KC>
-void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, const float* q3, int nq,
-                 int kl, int G, int nqt, float* cs, int* ci, hipStream_t s) {
+void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq, int kl, int G,
+                 int nqt, float* cs, int* ci, hipStream_t s) {
   if (kind == SCAN_BF16) {
     if (wide)
       launch_search<SearchWideBF, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
@@ -649,8 +704,8 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, const 
     return;
   }
   if constexpr (KC <= 16) {  // (a 64-entry list spills next to the x6 operands)
-    if (kind == SCAN_X6 && wide && q3) {
-      launch_search<SearchWideX6, KC>(ix, q3, nq, kl, G, nqt, cs, ci, s);
+    if (kind == SCAN_X6 && wide) {
+      launch_search<SearchWideX6, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
       return;
     }
   }
@@ -666,13 +721,13 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, const 
 // batch is re-scanned with 64-entry lists, so results are exact either way.  The
 // check costs one 4-byte device->host read, i.e. k > 16 calls are synchronous.
 int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* os, int64_t* oi,
-              hipStream_t s, const float* q3 = nullptr) {
+              hipStream_t s) {
   int kc = kc_scan(k);
   for (;;) {
     const int kl = std::min(kc, k);
     const bool check = kl < k;
     SearchPlan p = plan_search(ix, nq, kc);
-    if (kind == SCAN_STREAM) p.n_lists = (int64_t)stream_blocks(ix) * 16;
+    if (kind == SCAN_STREAM) p.n_lists = stream_blocks(ix);  // one list per block
     const size_t n_cand = (size_t)p.n_lists * nq * kl;
     int rc = ix->cand_s.ensure(n_cand * sizeof(float));
     if (!rc) rc = ix->cand_i.ensure(n_cand * sizeof(int));
@@ -692,9 +747,9 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
         default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
       }
     } else switch (kc) {
-      case 8: launch_scan<8>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
-      case 16: launch_scan<16>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
-      default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, q3, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      case 8: launch_scan<8>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      case 16: launch_scan<16>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
+      default: launch_scan<MQ_MAX_K>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
     }
     MQ_HIP(hipGetLastError());
     ix->tl.mark(s, 1);
@@ -762,22 +817,7 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
-  if (ix->precision == MQ_DTYPE_F32X6 && nq > 64 && ix->dim % 16 == 0) {
-    // split-f32 scan on P3 operands: mirror rows added since the last one, split queries
-    const int64_t w3 = (int64_t)ix->dim * 3 / 2;
-    int rc = ix->rows3.ensure((size_t)ix->cap * w3 * sizeof(float));
-    if (!rc) rc = ix->q3.ensure((size_t)nq * w3 * sizeof(float));
-    if (rc) return rc;
-    if (ix->n3 < ix->n) {
-      launch_split_p3(ix->rows + ix->n3 * ix->dim, ix->dim, ix->n - ix->n3, ix->dim,
-                      ix->rows3.as<float>() + ix->n3 * w3, s);
-      ix->n3 = ix->n;
-    }
-    launch_split_p3(q, ix->dim, nq, ix->dim, ix->q3.as<float>(), s);
-    MQ_HIP(hipGetLastError());
-    return scan_topk(ix, SCAN_X6, q, nq, k, os, oi, s, ix->q3.as<float>());
-  }
-  return scan_topk(ix, SCAN_F32, q, nq, k, os, oi, s);
+  return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
 }
 
 int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
@@ -795,8 +835,7 @@ int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
   if (ix->rows) MQ_HIP(hipFree(ix->rows));
   ix->rows = fresh;
   ix->cap = new_cap;
-  ix->n16 = 0;  // the bf16 / P3 shadows are rebuilt at the next search that needs them
-  ix->n3 = 0;
+  ix->n16 = 0;  // the bf16 shadow is rebuilt at the next coarse search
   return MQ_OK;
 }
 
@@ -852,8 +891,6 @@ int mq_index_destroy(mq_index* ix) {
     ix->out_i.release();
     ix->rows16.release();
     ix->q16.release();
-    ix->rows3.release();
-    ix->q3.release();
     ix->coarse_s.release();
     ix->coarse_i.release();
     ix->flag.release();
@@ -889,7 +926,6 @@ int mq_index_reset(mq_index* ix) {
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->n = 0;
   ix->n16 = 0;
-  ix->n3 = 0;
   return MQ_OK;
 }
 
@@ -922,6 +958,51 @@ int mq_index_add(mq_index* ix, const float* rows, int64_t n, int rows_on_device,
     if (!rows_on_device) MQ_HIP(hipStreamSynchronize(s));
   }
   ix->n += n;
+  return MQ_OK;
+}
+
+int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst) {
+  clear_error();
+  MQ_CHECK_ARG(src && dst, "NULL index");
+  MQ_CHECK_ARG(n >= 0 && (n == 0 || rows), "bad row list");
+  MQ_CHECK_ARG(src->dim == dst->dim, "dim mismatch (%d vs %d)", src->dim, dst->dim);
+  MQ_CHECK_ARG(src->device == dst->device, "indexes live on different devices");
+  std::unique_lock<std::mutex> l1(src->mu, std::defer_lock), l2(dst->mu, std::defer_lock);
+  if (src == dst)
+    l1.lock();
+  else
+    std::lock(l1, l2);
+  for (int64_t i = 0; i < n; ++i)
+    MQ_CHECK_ARG(rows[i] >= 0 && rows[i] < src->n, "row %lld out of range (n=%lld)",
+                 (long long)rows[i], (long long)src->n);
+  DeviceGuard dg(src->device);
+  float* fresh = nullptr;
+  int64_t* sel = nullptr;
+  if (n > 0) {
+    if (hipMalloc((void**)&fresh, (size_t)n * src->dim * sizeof(float)) != hipSuccess)
+      MQ_FAIL(MQ_ENOMEM, "hipMalloc of %lld rows failed", (long long)n);
+    if (hipMalloc((void**)&sel, (size_t)n * sizeof(int64_t)) != hipSuccess) {
+      (void)hipFree(fresh);
+      MQ_FAIL(MQ_ENOMEM, "hipMalloc of the row list failed");
+    }
+    hipError_t e = hipMemcpy(sel, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, nullptr,
+                         src->rows, sel, n, src->dim, fresh);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipFree(sel);
+    if (e != hipSuccess) {
+      (void)hipFree(fresh);
+      MQ_FAIL(MQ_EHIP, "row gather failed: %s", hipGetErrorString(e));
+    }
+  }
+  if (dst->rows) MQ_HIP(hipFree(dst->rows));
+  dst->rows = fresh;
+  dst->cap = n;
+  dst->n = n;
+  dst->n16 = 0;
   return MQ_OK;
 }
 
@@ -1066,7 +1147,6 @@ int mq_index_load(mq_index* ix, const char* path) {
   }
   ix->n = 0;
   ix->n16 = 0;
-  ix->n3 = 0;
   int rc = reserve_rows(ix, h.n_rows, nullptr);
   if (rc) {
     fclose(f);

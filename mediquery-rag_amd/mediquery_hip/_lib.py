@@ -59,6 +59,7 @@ SIGNATURES = {
     "mq_index_reset": (_I, [_P]),
     "mq_index_search": (_I, [_P, _P, _I64, _I, _P, _P, _I, _P]),
     "mq_index_get": (_I, [_P, _I64, _I64, _P, _I, _P]),
+    "mq_index_select": (_I, [_P, _P, _I64, _P]),
     "mq_index_data": (_I, [_P, _PP]),
     "mq_index_set_precision": (_I, [_P, _I]),
     "mq_index_set_stream_threshold": (_I, [_P, _I]),
@@ -84,8 +85,6 @@ SIGNATURES = {
     "mq_tokenizer_encode_batch": (_I, [_P, ctypes.POINTER(ctypes.c_char_p), _I, _I, _P, _P,
                                        ctypes.POINTER(_I)]),
     "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
-    "mq_debug_split_p3": (_I, [_P, _I64, _I64, _I, _P, _P]),
-    "mq_debug_split_p3t": (_I, [_P, _I64, _I64, _I, _P, _P]),
 }
 
 _lib = None

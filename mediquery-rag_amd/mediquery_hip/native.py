@@ -67,6 +67,14 @@ class FlatIndex:
         _lib.call("mq_index_get", self._h, row0, n, _lib.ptr(out), 0, None)
         return out
 
+    def select(self, rows, out=None):
+        """Index whose row i is this index's row rows[i] (device gather, no host copy of
+        the slab); out=self compacts in place.  Returns `out` (a new index if None)."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1)
+        out = FlatIndex(dim=self.dim, device=self.device) if out is None else out
+        _lib.call("mq_index_select", self._h, _lib.ptr(rows), rows.size, out._h)
+        return out
+
     def data_ptr(self):
         p = ctypes.c_void_p()
         _lib.call("mq_index_data", self._h, ctypes.byref(p))

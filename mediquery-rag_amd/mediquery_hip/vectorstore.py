@@ -158,10 +158,7 @@ class HipChroma(VectorStoreBase):
             return None
         drop = set(ids)
         keep = [r for r, i in enumerate(self._ids) if i not in drop]
-        rows = self._index.get()[keep] if keep else np.zeros((0, self._dim), np.float32)
-        self._index.reset()
-        if len(rows):
-            self._index.add(rows)  # already unit-norm: re-normalising is the identity
+        self._index.select(keep, out=self._index)  # device compaction, rows bit-identical
         self._ids = [self._ids[r] for r in keep]
         self._texts = [self._texts[r] for r in keep]
         self._metas = [self._metas[r] for r in keep]
@@ -198,9 +195,9 @@ class HipChroma(VectorStoreBase):
         allowed = np.array([r for r in range(n) if _match(self._metas[r], filter)], dtype=np.int64)
         if len(allowed) == 0:
             return []
-        # exact filtered search: score only the allowed rows in a scratch device index
-        sub = FlatIndex(dim=self._dim, device=self._device)
-        sub.add(self._index.get()[allowed])
+        # exact filtered search: score only the allowed rows, gathered on the device into
+        # a scratch index (rows bit-identical to the store's)
+        sub = self._index.select(allowed)
         kk = min(k, len(allowed), _lib.MQ_MAX_K)
         s, i = sub.search(q, kk)
         sub.close()

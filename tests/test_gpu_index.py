@@ -268,3 +268,27 @@ def test_large_k_list_overflow_rescan(require_gpu, prec, nq):
         if prec != _lib.MQ_DTYPE_BF16:
             ref = exact_scores(q, c)
             assert check_topk(i, s, ref, k) == []
+
+
+def test_select_gathers_and_compacts(require_gpu):
+    """mq_index_select: device gather of chosen rows (any order, repeats) into another
+    index, and in-place compaction; rows come back bit-identical, search follows."""
+    c = synth.corpus(3000, 768, clustered=True)
+    ix = _index(c)
+    stored = ix.get()
+    sel = np.array([2999, 5, 5, 17, 0, 1234], np.int64)
+    sub = ix.select(sel)
+    assert len(sub) == len(sel)
+    np.testing.assert_array_equal(sub.get(), stored[sel])
+    s, i = sub.search(stored[[17]], 2)
+    assert i[0, 0] == 3 and i[0, 1] != 3
+    keep = np.arange(0, 3000, 3)
+    ix.select(keep, out=ix)
+    assert len(ix) == len(keep)
+    np.testing.assert_array_equal(ix.get(), stored[keep])
+    ix.add(c[:2])  # grows again after a compaction
+    assert len(ix) == len(keep) + 2
+    ix.select([], out=ix)
+    assert len(ix) == 0
+    with pytest.raises(_lib.MQError, match="out of range"):
+        sub.select([6])

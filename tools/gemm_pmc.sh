@@ -2,7 +2,7 @@
 # PMC passes over selected GEMM tiles (run via gpurun from the repo root):
 #   bash tools/gemm_pmc.sh <tag> <shapes> <tiles>
 set -euo pipefail
-TAG=${1:-g}; SHAPES=${2:-qkv,ffn_up}; TILES=${3:-1,6,14}
+TAG=${1:-g}; SHAPES=${2:-qkv,ffn_up}; TILES=${3:-1,6}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_$TAG
 mkdir -p "$OUT"

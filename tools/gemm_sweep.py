@@ -1,4 +1,4 @@
-"""Time the MFMA GEMM core (exact f32, split-f32, split-f32 on P3 operands) per tile geometry on the encoder's shapes (B=256, L=32)
+"""Time the fp32 MFMA GEMM core per tile geometry on the encoder's shapes (B=256, L=32)
 through the mq_debug_gemm_f32 hook.  Prints TFLOP/s per (shape, tile)."""
 import json
 import os
@@ -11,11 +11,11 @@ from mediquery_hip import _lib  # noqa: E402
 
 SHAPES = {"qkv": (8192, 2304, 768), "out_proj": (8192, 768, 768), "ffn_up": (8192, 3072, 768),
           "ffn_down": (8192, 768, 3072)}
-TILES = {0: "f32_128x128", 1: "f32_128x96", 2: "f32_128x64", 3: "f32_32x128", 5: "x6_128x128", 6: "x6_128x96", 7: "x6_128x64", 8: "p3_128x128", 9: "p3_128x96", 10: "p3_128x64", 11: "p3out_128x128", 12: "p3out_128x96", 13: "p3out_128x64", 14: "wide_256x96", 15: "wide_256x128", 16: "wideout_256x96", 17: "wideout_256x128"}
+TILES = {0: "f32_128x128", 1: "f32_128x96", 2: "f32_128x64", 3: "f32_32x128", 5: "x6_128x128", 6: "x6_128x96", 7: "x6_128x64"}
 
 
 def main():
-    # optional filters: --shapes qkv,ffn_up --tiles 1,6,14 --iters 20
+    # optional filters: --shapes qkv,ffn_up --tiles 1,6 --iters 20
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default=",".join(SHAPES))
@@ -32,25 +32,11 @@ def main():
         b = torch.randn(N, device=dev)
         R = torch.randn(M, N, device=dev)
         out = torch.empty(M, N, device=dev)
-        A3 = torch.empty(M, K * 3 // 2, device=dev)
-        W3 = torch.empty(N, K * 3 // 2, device=dev)
-        _lib.call("mq_debug_split_p3", _lib.ptr(A), K, M, K, _lib.ptr(A3), _lib.stream_handle())
-        _lib.call("mq_debug_split_p3", _lib.ptr(W), K, N, K, _lib.ptr(W3), _lib.stream_handle())
-        A3t = torch.empty((M + 31) // 32 * 32 * K * 3 // 2, device=dev)
-        W3t = torch.empty((N + 31) // 32 * 32 * K * 3 // 2, device=dev)
-        _lib.call("mq_debug_split_p3t", _lib.ptr(A), K, M, K, _lib.ptr(A3t), _lib.stream_handle())
-        _lib.call("mq_debug_split_p3t", _lib.ptr(W), K, N, K, _lib.ptr(W3t), _lib.stream_handle())
         epi = 1 if name == "ffn_up" else (3 if name in ("out_proj", "ffn_down") else 0)
         for t, tname in tiles.items():
-            p3out = t in (11, 12, 13, 16, 17)
-            if p3out and (epi == 3 or N % 16):
-                continue
-            o = torch.empty((M + 31) // 32 * 32, N * 3 // 2, device=dev) if p3out else out
-            a, w = (A3t, W3t) if t >= 14 else ((A3, W3) if t >= 8 else (A, W))
-
             def run():
-                _lib.call("mq_debug_gemm_f32", _lib.ptr(a), _lib.ptr(w), _lib.ptr(b), _lib.ptr(R),
-                          _lib.ptr(o), M, N, K, epi, t, _lib.stream_handle())
+                _lib.call("mq_debug_gemm_f32", _lib.ptr(A), _lib.ptr(W), _lib.ptr(b), _lib.ptr(R),
+                          _lib.ptr(out), M, N, K, epi, t, _lib.stream_handle())
             for _ in range(3):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
