@@ -72,6 +72,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     int64_t n0l;
     coords(i, m0, n0l);
     const int n0 = (int)n0l;
+    if (m0 + T::BM <= M && n0 + T::BN <= N) {
+      // full tile: every bias / residual load goes out before the first use, so the
+      // tile pays one memory round trip (the guarded loop below waits per element)
+      float bv[T::TN];
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn) bv[tn] = bias[n0 + wn * T::WN + tn * 32 + (lane & 31)];
+      float rv[T::TM][T::TN][16];
+      if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              rv[tm][tn][e] = resid[(int64_t)(m0 + wm * T::WM + acc_row(tm, e, lane)) * ldr + n0 +
+                                    wn * T::WN + tn * 32 + (lane & 31)];
+      }
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float v = acc[tm][tn][e] + bv[tn];
+            if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+            if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+            if (EPI == EPI_RESID) v += rv[tm][tn][e];
+            out[(int64_t)(m0 + wm * T::WM + acc_row(tm, e, lane)) * ldo + n0 + wn * T::WN + tn * 32 +
+                (lane & 31)] = v;
+          }
+      return;
+    }
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn) {
       const int col = n0 + wn * T::WN + tn * 32 + (lane & 31);
