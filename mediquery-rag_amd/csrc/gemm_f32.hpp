@@ -308,7 +308,9 @@ __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOp
       // them (WAW)
       __builtin_amdgcn_sched_barrier(0);
       float* cur = lds + (j & 1) * T::STAGE_FLOATS;
+      __builtin_amdgcn_s_setprio(1);
       mma_slice<T>(cur, acc, wm, wn, lane);
+      __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       st[(d + 1) % D].store(lds + ((j + 1) & 1) * T::STAGE_FLOATS, tid);
       __syncthreads();
