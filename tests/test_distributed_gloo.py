@@ -1,6 +1,7 @@
-"""Row-sharded search across processes (world_size 2, gloo, CPU): the all-gather of
-per-shard candidates plus the merge must equal the single-index exact answer.  The
-per-shard local search here is the oracle; on GPUs it is the K9/K10 kernels."""
+"""Row-sharded search across processes (world_size 2 and 3, gloo, CPU): the all-gather
+of per-shard candidates plus the merge must equal the single-index exact answer,
+including uneven shards and k larger than a shard (padding candidates).  The per-shard
+local search here is the oracle; on GPUs it is the K9/K10 kernels."""
 import os
 import socket
 
@@ -10,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-N, DIM, NQ, K = 997, 64, 12, 7
+DIM, NQ = 64, 12
 
 
 def _free_port():
@@ -21,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, N, K):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "mediquery-rag_amd"), root]
@@ -36,8 +37,12 @@ def _worker(rank, world, port, out_q):
         shard = c[off:off + cnt]
 
         def local(q, k):
+            # the device contract (mq_index_search): [nq, k], padded with (-inf, -1)
             s, i = search(q.numpy(), shard, k)
-            return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(i)
+            ps = np.full((q.shape[0], k), -np.inf, np.float32)
+            pi = np.full((q.shape[0], k), -1, np.int64)
+            ps[:, :s.shape[1]], pi[:, :i.shape[1]] = s, i
+            return torch.from_numpy(ps), torch.from_numpy(pi)
 
         ss = ShardedSearcher(local, off)
         q, _ = synth.queries(NQ, c)
@@ -53,14 +58,14 @@ def _worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def test_sharded_search_equals_single_index():
+@pytest.mark.parametrize("world,N,K", [(2, 997, 7), (3, 1000, 5), (3, 10, 7)])
+def test_sharded_search_equals_single_index(world, N, K):
     from mediquery_hip import synth
     from oracle.flat import exact_scores, check_topk
-    world = 2
     ctx = mp.get_context("spawn")
     q_out = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q_out)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q_out, N, K)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q_out.get(timeout=120) for _ in range(world)]
@@ -77,4 +82,5 @@ def test_sharded_search_equals_single_index():
         assert check_topk(ids, scores, ref, K) == []
         half = NQ // world
         np.testing.assert_array_equal(ids_dp, ids[rank * half:(rank + 1) * half])
-    np.testing.assert_array_equal(res[0][1], res[1][1])
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][1], r[1])
