@@ -51,12 +51,15 @@ class ShardedSearcher:
         g = self._all_gather(q_local)
         return g.reshape(-1, q_local.shape[-1])
 
-    def search(self, queries, k):
-        """Global top-k of `queries` (identical on every rank) over all shards."""
+    def search(self, queries, k, keep=None):
+        """Global top-k of `queries` (identical on every rank) over all shards; with
+        keep=(start, stop) only those query rows are merged and returned."""
         s, i = self.local_search(queries, k)
         i = torch.where(i >= 0, i + self.offset, i)
         gs, gi = self._all_gather(s), self._all_gather(i)  # [world, nq, k]
-        nq = queries.shape[0]
+        if keep is not None:
+            gs, gi = gs[:, keep[0]:keep[1]].contiguous(), gi[:, keep[0]:keep[1]].contiguous()
+        nq = gs.shape[1]
         if gs.is_cuda:
             os_ = torch.empty((nq, k), dtype=torch.float32, device=gs.device)
             oi = torch.empty((nq, k), dtype=torch.int64, device=gs.device)
@@ -69,6 +72,5 @@ class ShardedSearcher:
         """DP-encoded queries: gather every rank's batch, search all, keep own rows."""
         world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
         allq = self.gather_queries(q_local)
-        s, i = self.search(allq, k)
         B = q_local.shape[0]
-        return s[rank * B:(rank + 1) * B], i[rank * B:(rank + 1) * B]
+        return self.search(allq, k, keep=(rank * B, (rank + 1) * B))  # merge own rows only
