@@ -196,6 +196,34 @@ def main():
     enc.set_precision(PRECISIONS["f32"])
     index.set_precision(PRECISIONS["f32"])
 
+    # ---- BASELINE config 5 beside it: bf16 index scanned as an MFMA GEMM for the top 64
+    # (k=50 -> max(2k,50) capped at 64) + exact fp32 re-rank; search only, same queries,
+    # recall@50 against the exact fp32 scan ---------------------------------------------
+    cfg5 = None
+    if world == 1:
+        k5 = 50
+        s5 = torch.empty((B, k5), dtype=torch.float32, device=dev)
+        i5 = torch.empty((B, k5), dtype=torch.int64, device=dev)
+        index.search_device(q, k5, s5, i5)
+        exact = i5.clone()
+        index.set_precision(_lib.MQ_DTYPE_BF16)
+        index.search_device(q, k5, s5, i5)  # builds the bf16 shadow slab (untimed)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            index.search_device(q, k5, s5, i5)
+        e1.record()
+        torch.cuda.synchronize()
+        ms5 = e0.elapsed_time(e1) / 10
+        hits = sum(len(set(a) & set(b)) for a, b in zip(i5.cpu().tolist(), exact.cpu().tolist()))
+        cfg5 = {"workload": "BASELINE config 5 (search only): %d x 768 bf16 shadow slab, batch %d, "
+                            "bf16 MFMA coarse top-64 + exact fp32 re-rank to k=%d" % (cnt, B, k5),
+                "queries_per_s": round(B / ms5 * 1e3, 1), "ms_per_batch": round(ms5, 3),
+                "recall_at_k_vs_exact_f32": round(hits / (B * k5), 5),
+                "hbm_gbs_algorithmic": round(cnt * 768 * 2 / (ms5 * 1e-3) / 1e9, 1)}
+        index.set_precision(PRECISIONS["f32"])
+
     # ---- single-query latency (embed 1 query + search the shard), exact f32 ----------
     lat = []
     if world == 1 and args.single_iters > 0:
@@ -289,6 +317,7 @@ def main():
         "split_f32": dict(alt_r, dtype="f32 via exact 3-way bf16 split (6 bf16 MFMAs / product, "
                                        "fp32 accumulate); same parity tolerances as f32"),
     }
+    out["config5_bf16_rerank"] = cfg5
     if world == 1 and not args.no_cpu_baseline:
         def corpus_host():
             return torch.nn.functional.normalize(

@@ -186,7 +186,8 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
  * epi 0 bias, 1 bias+GELU(erf), 2 bias+GELU(tanh), 3 bias+residual; tile 0 = 128x128,
  * 1 = 128x96, 2 = 128x64, 3 = 32x128 (exact f32), 4 = split-K (32x128 tiles + ordered
  * slab reduction; synchronous, N % 4 == 0), 5-7 = split-f32 (x6) 128x128 / 128x96 /
- * 128x64.  K % 32 == 0.  For kernel unit tests. */
+ * 128x64, 8 / 9 = exact / split-f32 128x192 on 8-wave workgroups.  K % 32 == 0.  For
+ * kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
 

@@ -48,7 +48,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // Within a round, the workgroups of one XCD (blockIdx % 8 equal) take consecutive
 // tiles, i.e. share A row panels in their L2.
 template <class T, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, int lda,
+__global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ resid, int ldr,
@@ -502,9 +502,9 @@ struct GemmArgs {
 template <class T, int EPI>
 void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s) {
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-  // persistent grid: at most two workgroups per CU, rounded up to a multiple of 8
-  const int grid = (std::min(tiles, 2 * num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(256), 0, s, g.A, g.lda, g.W,
+  // persistent grid: the workgroups that fit the CUs at once, a multiple of 8
+  const int grid = (std::min(tiles, T::WG_PER_CU * num_cus) + 7) / 8 * 8;
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda, g.W,
                      g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
 }
 
@@ -523,7 +523,8 @@ using X6Mid = F32Tile<2, 2, 2, 1, true>;  // 128 x 64
 
 // Tile codes (also the mq_debug_gemm_f32 `tile` argument): 0-3 exact f32 128x128 /
 // 128x96 / 128x64 / 32x128, 4 split-K (host path only), 5-7 split-f32 128x128 / 128x96
-// / 128x64.
+// / 128x64, 8 / 9 exact / split-f32 128x192 with 8-wave workgroups (one per CU; measured
+// within run-to-run noise of the 4-wave tiles, kept as a test of the 8-wave walker).
 template <int EPI>
 void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
   switch (tile) {
@@ -533,6 +534,8 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
     case 5: launch_gemm_t<X6Big, EPI>(g, num_cus, s); return;
     case 6: launch_gemm_t<X6T96, EPI>(g, num_cus, s); return;
     case 7: launch_gemm_t<X6Mid, EPI>(g, num_cus, s); return;
+    case 8: launch_gemm_t<F32Tile<4, 2, 1, 3>, EPI>(g, num_cus, s); return;         // 128x192, 8 waves
+    case 9: launch_gemm_t<F32Tile<4, 2, 1, 3, true>, EPI>(g, num_cus, s); return;   // x6 128x192
     default: launch_gemm_t<GemmSmall, EPI>(g, num_cus, s); return;
   }
 }
@@ -908,7 +911,7 @@ int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % kBK == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 7, "bad epi/tile");
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= 0 && tile <= 9, "bad epi/tile");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -19,8 +19,8 @@
 //    (112-B rows: slot = 7*row + 2*plane + h mod 16, conflict-free); lane half h carries
 //    k = 8h + j.
 //
-//  * 256 threads = 4 waves laid out WAVES_M x WAVES_N; each wave owns TM x TN MFMA
-//    tiles of 32x32 (f32x16 accumulators, 16 regs/lane each).
+//  * 256 or 512 threads = 4 or 8 waves laid out WAVES_M x WAVES_N; each wave owns
+//    TM x TN MFMA tiles of 32x32 (f32x16 accumulators, 16 regs/lane each).
 //  * Global loads run two slices ahead in two named register stages (walk_tiles).
 #pragma once
 
@@ -56,7 +56,9 @@ struct F32Tile {
   static constexpr int LOADS = (TOTAL_F4 + THREADS - 1) / THREADS;      // per thread
   static constexpr bool PARTIAL = TOTAL_F4 % THREADS != 0;              // last slot ragged
   static constexpr int STAGE_FLOATS = ROWS * ROW_FLOATS;
-  static_assert(THREADS == 256, "tile core assumes 256-thread workgroups");
+  static_assert(THREADS == 256 || THREADS == 512, "4- or 8-wave workgroups");
+  // workgroups per CU the kernel is built for: 2 x 4 waves, or 1 x 8 waves (LDS)
+  static constexpr int WG_PER_CU = THREADS == 256 ? 2 : 1;
   static_assert(BM % 32 == 0 && BN % 32 == 0, "block tile must be a multiple of 32");
   static_assert((BM * F4_PER_ROW) % THREADS == 0, "A / B rows must not share a load slot");
 };

@@ -1,7 +1,7 @@
 """Unit tests of the MFMA GEMM core (gemm_f32.hpp) behind every encoder projection:
 each tile geometry x epilogue on ragged shapes against a float64 torch reference
-(|err| <= 2e-5 * sqrt(K) relative to the row/col norms), for the exact-f32 tiles (0-4)
-and the split-f32 tiles (5-7)."""
+(|err| <= 2e-5 * sqrt(K) relative to the row/col norms), for the exact-f32 tiles (0-4),
+the split-f32 tiles (5-7) and the 8-wave workgroup tiles (8-9)."""
 import math
 
 import numpy as np
@@ -28,7 +28,7 @@ def torch_erf(x):
     return torch.erf(x)
 
 
-@pytest.mark.parametrize("tile", list(range(8)))
+@pytest.mark.parametrize("tile", list(range(10)))
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(1, 768, 768), (77, 96, 64), (300, 2304, 768),
                                    (1000, 768, 3072), (4099, 200, 32), (32, 3072, 768), (256, 768, 3072)])

@@ -11,7 +11,7 @@ from mediquery_hip import _lib  # noqa: E402
 
 SHAPES = {"qkv": (8192, 2304, 768), "out_proj": (8192, 768, 768), "ffn_up": (8192, 3072, 768),
           "ffn_down": (8192, 768, 3072)}
-TILES = {0: "f32_128x128", 1: "f32_128x96", 2: "f32_128x64", 3: "f32_32x128", 5: "x6_128x128", 6: "x6_128x96", 7: "x6_128x64"}
+TILES = {0: "f32_128x128", 1: "f32_128x96", 2: "f32_128x64", 3: "f32_32x128", 5: "x6_128x128", 6: "x6_128x96", 7: "x6_128x64", 8: "f32w_128x192", 9: "x6w_128x192"}
 
 
 def main():
