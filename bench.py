@@ -35,9 +35,13 @@ from mediquery_hip.distributed import ShardedSearcher, shard_bounds  # noqa: E40
 from mediquery_hip.native import Encoder, FlatIndex  # noqa: E402
 from mediquery_hip import _lib  # noqa: E402
 
-# the headline is measured on the exact f32 MFMA path; the split-f32 path is timed in
-# the same run and reported beside it
-PRECISIONS = {"f32": _lib.MQ_DTYPE_F32, "f32x6": _lib.MQ_DTYPE_F32X6}
+# run name -> (encoder arithmetic, search mode).  The headline "f32" computes exact fp32
+# results: the encoder on the f32 MFMA, the top-k by the certified screen (split-f32 scan
+# for k+3 candidates, fp32 re-rank, proven bound, direct exact scan on failure).  The same
+# run times the direct exact scan ("f32_direct_search") and the all-split-f32 variant.
+PRECISIONS = {"f32": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32_SCREEN),
+              "f32_direct_search": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32),
+              "f32x6": (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32X6)}
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
@@ -149,18 +153,19 @@ def main():
     # parity guard at full size: planted queries find their rows (property check)
     pq, planted = synth.queries_device(64, full)
     ok_planted = {}
-    for name, prec in PRECISIONS.items():
+    for name, (_, prec) in PRECISIONS.items():
         index.set_precision(prec)
         _, pq_i = searcher.search(pq, K) if world > 1 else local_search(pq, K)
         ok_planted[name] = bool((pq_i[:32, 0] == planted[:32]).all())
     del full
     torch.cuda.empty_cache()
 
-    def measure(prec):
+    def measure(precs):
         """Warm up, then time exactly args.steps steps (barrier + sync on both sides,
         max over ranks); per-kernel-class device time from HIP events."""
-        enc.set_precision(prec)
-        index.set_precision(prec)
+        enc.set_precision(precs[0])
+        index.set_precision(precs[1])
+        fb0 = index.screen_fallbacks
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         for _ in range(args.warmup):
             step()
@@ -188,13 +193,13 @@ def main():
         stage_ms.update({k: v / args.steps for k, v in index.read_timing().items()})
         enc.set_timing(False)
         index.set_timing(False)
-        return {"elapsed": elapsed, "stage_ms": stage_ms,
+        return {"elapsed": elapsed, "stage_ms": stage_ms, "screen_fallbacks": index.screen_fallbacks - fb0,
                 "enc_ms": statistics.mean(e[0].elapsed_time(e[1]) for e in evs),
                 "srch_ms": statistics.mean(e[1].elapsed_time(e[2]) for e in evs)}
 
-    runs = {name: measure(prec) for name, prec in PRECISIONS.items()}
-    enc.set_precision(PRECISIONS["f32"])
-    index.set_precision(PRECISIONS["f32"])
+    runs = {name: measure(precs) for name, precs in PRECISIONS.items()}
+    enc.set_precision(_lib.MQ_DTYPE_F32)
+    index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
 
     # ---- BASELINE config 5 beside it: bf16 index scanned as an MFMA GEMM for the top 64
     # (k=50 -> max(2k,50) capped at 64) + exact fp32 re-rank; search only, same queries,
@@ -222,7 +227,7 @@ def main():
                 "queries_per_s": round(B / ms5 * 1e3, 1), "ms_per_batch": round(ms5, 3),
                 "recall_at_k_vs_exact_f32": round(hits / (B * k5), 5),
                 "hbm_gbs_algorithmic": round(cnt * 768 * 2 / (ms5 * 1e-3) / 1e9, 1)}
-        index.set_precision(PRECISIONS["f32"])
+        index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
 
     # ---- single-query latency (embed 1 query + search the shard), exact f32 ----------
     lat = []
@@ -263,38 +268,46 @@ def main():
             traffic_db = {}
     srch_bytes = cnt * 768 * 4 + nq_all * 768 * 4 + nq_all * K * 12
 
+    X6_PEAK = BF16_PEAK_TFLOPS / 6.0  # six bf16 MFMAs per fp32 product: 417 TFLOP/s fp32-equiv.
+
     def summarize(name, r):
-        # x6 issues six bf16 MFMAs per fp32 product: its hardware roof is the dense bf16
-        # MFMA peak over 6x the algorithmic FLOPs (= 417 TFLOP/s fp32-equivalent)
-        peak = FP32_PEAK_TFLOPS if name == "f32" else BF16_PEAK_TFLOPS / 6.0
+        enc_x6 = PRECISIONS[name][0] == _lib.MQ_DTYPE_F32X6
+        scan_x6 = PRECISIONS[name][1] in (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32_SCREEN)
         kernels = {}
         for kname, ms in r["stage_ms"].items():
             d = {"ms_per_step": round(ms, 4)}
             if kname in flops and ms > 0:
+                pk = (scan_x6 if kname == "flat_search_kernel" else enc_x6) and X6_PEAK or FP32_PEAK_TFLOPS
                 tf = flops[kname] / (ms * 1e-3) / 1e12
-                d.update(tflops=round(tf, 2), frac_peak=round(tf / peak, 4))
+                d.update(tflops=round(tf, 2), frac_peak=round(tf / pk, 4))
             kernels[kname] = d
         dom = max((n for n in flops if r["stage_ms"].get(n, 0) > 0), key=lambda n: r["stage_ms"][n])
+        dom_x6 = scan_x6 if dom == "flat_search_kernel" else enc_x6
+        peak = X6_PEAK if dom_x6 else FP32_PEAK_TFLOPS
         dom_tf = flops[dom] / (r["stage_ms"][dom] * 1e-3) / 1e12
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(dom_tf, 2), "peak": round(peak, 1),
-                "unit": "TFLOP/s" if name == "f32" else "TFLOP/s (fp32-equivalent)",
+                "unit": "TFLOP/s (fp32-equivalent)" if dom_x6 else "TFLOP/s",
                 "frac": round(dom_tf / peak, 4),
-                "traffic": traffic_db.get(dom) if name == "f32" else None}
+                "traffic": None if dom_x6 else traffic_db.get(dom)}
         sk = r["stage_ms"].get("flat_search_kernel", r["srch_ms"])
-        search_roof = {"kernel": "flat_search_kernel", "bound": "mfma",
+        speak = X6_PEAK if scan_x6 else FP32_PEAK_TFLOPS
+        search_roof = {"kernel": "flat_search_kernel (%s)" % ("split-f32" if scan_x6 else "exact f32"),
+                       "bound": "mfma",
                        "achieved_tflops": kernels.get("flat_search_kernel", {}).get("tflops"),
-                       "peak": round(peak, 1),
+                       "peak": round(speak, 1),
                        "hbm_gbs_algorithmic": round(srch_bytes / (sk * 1e-3) / 1e9, 1),
                        "hbm_frac": round(srch_bytes / (sk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        "bytes_per_launch": srch_bytes, "flops_per_launch": flops["flat_search_kernel"],
-                       "traffic": traffic_db.get("flat_search_kernel") if name == "f32" else None}
+                       "traffic": None if scan_x6 else traffic_db.get("flat_search_kernel")}
         return {"value": round(nq_all * args.steps / r["elapsed"], 2),
                 "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
                 "roofline": roof, "search_roofline": search_roof,
                 "encoder_ms": round(r["enc_ms"], 3), "search_ms": round(r["srch_ms"], 3),
-                "kernels": kernels, "planted_top1_ok": ok_planted[name]}
+                "kernels": kernels, "planted_top1_ok": ok_planted[name],
+                "screen_fallbacks": r["screen_fallbacks"]}
 
     main_r = summarize("f32", runs["f32"])
+    direct_r = summarize("f32_direct_search", runs["f32_direct_search"])
     alt_r = summarize("f32x6", runs["f32x6"])
     out = {
         "metric": "queries/s (embed+top-k, k=5, b=256) over 1M×768 corpus; p50 single-query ms",
@@ -314,6 +327,11 @@ def main():
         "search_roofline": main_r["search_roofline"],
         "encoder_ms": main_r["encoder_ms"], "search_ms": main_r["search_ms"],
         "kernels": main_r["kernels"],
+        "search_mode": "exact fp32 top-k: split-f32 screen for k+3 candidates, fp32 re-rank, "
+                       "certified bound (direct exact scan when it fails; %d fallbacks in the timed "
+                       "steps)" % main_r["screen_fallbacks"],
+        "f32_direct_search": {kk: direct_r[kk] for kk in ("value", "ms_per_step", "search_ms",
+                                                          "search_roofline", "planted_top1_ok")},
         "split_f32": dict(alt_r, dtype="f32 via exact 3-way bf16 split (6 bf16 MFMAs / product, "
                                        "fp32 accumulate); same parity tolerances as f32"),
     }

@@ -46,6 +46,9 @@ extern "C" {
 #define MQ_DTYPE_BF16 1   /* bf16 storage (coarse paths)                                    */
 #define MQ_DTYPE_F32X6 2  /* fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMAs per
                            * product, fp32 accumulate: fp32-class error, 2.67x the MFMA rate */
+#define MQ_DTYPE_F32_SCREEN 3 /* search only: exact fp32 top-k at the F32X6 rate - split-f32
+                               * scan for k + 3..8 candidates, fp32 re-rank, certified bound
+                               * (else the direct exact scan); batches > 64, k <= 56 */
 
 #define MQ_GELU_ERF 0  /* exact erf GELU (HF BERT "gelu")            */
 #define MQ_GELU_TANH 1 /* tanh approximation (ggml / llama.cpp gelu)  */
@@ -96,7 +99,9 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
  * fp32, large batches; small batches stay on the exact kernel, HBM-bound there), or
  * MQ_DTYPE_BF16: bf16 shadow slab scanned on bf16 MFMA for the top max(k, 50) (capped
  * at MQ_MAX_K) candidates, then an exact fp32 re-rank to the top-k (BASELINE config 5;
- * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0. */
+ * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0.
+ * MQ_DTYPE_F32_SCREEN: exact fp32 results via the certified split-f32 screen (above);
+ * scores are the fp32 re-rank's dot products. */
 int mq_index_set_precision(mq_index* ix, int dtype);
 /* Batches of at most `max_queries` queries (default 4, 0..16; dim % 64 == 0, dim <= 1024)
  * use the streaming fp32 kernel instead of the MFMA tiles, whatever the precision. */
@@ -104,6 +109,9 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries);
 /* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
  * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
+/* Screened searches (MQ_DTYPE_F32_SCREEN) whose certificate failed and that were re-run
+ * on the direct exact scan. */
+int mq_index_screen_fallbacks(const mq_index* ix, int64_t* n);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
 /* Device-time accounting with HIP events on the launch stream (off by default).

@@ -233,29 +233,62 @@ __device__ __forceinline__ void ln_row_store(floatx4 (&x)[VPL], const float* __r
 
 // Split-K reduction of a residual projection fused with the LayerNorm after it (few-row
 // path: saves a launch and the y round trip per LN): x = LN(sum_s slab[s] + bias +
-// resid), one wave per row, slabs summed in order - bit-identical to
-// splitk_reduce_kernel<EPI_RESID> followed by ln_kernel.  A wave reads its whole row
-// before writing it, so dst may alias resid row for row (stride H).
+// resid), slabs summed in order (the LN's reductions are block-wide, so the result
+// matches splitk_reduce_kernel<EPI_RESID> + ln_kernel to rounding).  A block reads its
+// whole row before writing it, so dst may alias resid row for row (stride H).
 template <int VPL>
 __global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(
     const float* __restrict__ slab, int S, int M, const float* __restrict__ bias,
     const float* resid, int ldr, const float* __restrict__ g, const float* __restrict__ b,
     float eps, float* dst) {
+  // one 256-thread block per row (the few-row path has few rows: 4 waves per row keep
+  // 4x more slab loads in flight than a wave per row); thread t owns columns t + 256 i
   constexpr int H = VPL * 256;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  __shared__ float part[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int row = blockIdx.x;
   const int64_t plane = (int64_t)M * H;
-  floatx4 x[VPL];
+  float x[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    floatx4 v = sum_slabs(slab + (int64_t)row * H + c, plane, S);
-    v += *reinterpret_cast<const floatx4*>(bias + c);
-    v += *reinterpret_cast<const floatx4*>(resid + (int64_t)row * ldr + c);
-    x[i] = v;
+    const int c = t + 256 * i;
+    const float* p = slab + (int64_t)row * H + c;
+    float v = p[0];
+    int sl = 1;
+    for (; sl + 8 <= S; sl += 8) {
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = p[(sl + j) * plane];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v += u[j];
+    }
+    for (; sl < S; ++sl) v += p[sl * plane];
+    x[i] = v + bias[c] + resid[(int64_t)row * ldr + c];
   }
-  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, lane);
+  auto block_sum = [&](float v) {
+    v = wave_sum(v);
+    if (lane == 0) part[wave] = v;
+    __syncthreads();
+    const float r = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+    return r;
+  };
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) sum += x[i];
+  const float mean = block_sum(sum) * (1.0f / H);
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    x[i] -= mean;
+    var += x[i] * x[i];
+  }
+  const float rstd = 1.0f / sqrtf(block_sum(var) * (1.0f / H) + eps);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = t + 256 * i;
+    dst[(int64_t)row * H + c] = x[i] * rstd * g[c] + b[c];
+  }
 }
 
 // One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).
@@ -676,8 +709,8 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
     hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W, g.M,
                        g.N, g.K, S, g.slab);
     e->tl.mark(s, ST_LN);
-    hipLaunchKernelGGL((splitk_reduce_ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, g.slab, S, g.M, g.bias,
-                       g.resid, g.ldr, lng, lnb, e->cfg.ln_eps, x);
+    hipLaunchKernelGGL((splitk_reduce_ln_kernel<VPL>), dim3((unsigned)g.M), dim3(256), 0, s, g.slab, S,
+                       g.M, g.bias, g.resid, g.ldr, lng, lnb, e->cfg.ln_eps, x);
     return;
   }
   gemm<EPI_RESID>(e, g, stage, s);

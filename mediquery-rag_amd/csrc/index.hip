@@ -374,6 +374,33 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
+// Certificate of the screened exact search (MQ_DTYPE_F32_SCREEN).  The split-f32 scan
+// kept the kc best candidates of each query by its score s; a row r outside them has
+// s_r <= s_kc.  Every split-f32 score is within eps of the exact dot (dropped split
+// terms < 3 2^-24 |q||c| per product, fp32 accumulation over <= 64 x 6 MFMA steps:
+// <= 2.5e-5 ||q|| for unit rows and dim <= 1024) and so is every fp32 re-rank score
+// (<= 18 roundings), eps = 4e-5 ||q||.  Hence s_kc + 2 eps < e_k (the re-ranked k-th
+// score) proves no outside row can enter the exact top-k; otherwise flag the batch for
+// the direct exact scan.  One wave per query.
+__global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restrict__ Q, int dim,
+                                                            const float* __restrict__ cs, int kc,
+                                                            const float* __restrict__ es, int k,
+                                                            int64_t nq, int* __restrict__ flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
+  float ss = 0.f;
+  for (int i = lane; i < (dim >> 2); i += 64) {
+    const floatx4 v = q4[i];
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+  const float eps = 4e-5f * sqrtf(ss);
+  if (lane == 0 && !(cs[q * kc + kc - 1] + 2.f * eps < es[q * k + k - 1])) atomicOr(flag, 1);
+}
+
 // ======================================================= K10: merge lists ======
 // One block per query.  Each list is sorted, so a thread walks its share of the lists
 // (lists tid, tid+256, ...) reading heads in batches of 8 independent loads, and only
@@ -582,6 +609,7 @@ struct mq_index {
   DevBuf flag;          // merge overflow flag (k > 16)
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
   int64_t remerges = 0;  // merges re-run with 64-entry thread lists
+  int64_t screen_fallbacks = 0;  // screened searches whose certificate failed
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
@@ -808,6 +836,35 @@ int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* o
   return MQ_OK;
 }
 
+// Exact fp32 top-k at the split-f32 rate (MQ_DTYPE_F32_SCREEN, batches > 64): the
+// split-f32 scan keeps kc = k + 3..8 candidates per query, an fp32 re-rank orders them, and
+// screen_verify_kernel certifies that no other row can enter the top-k; a batch with
+// any uncertified query is re-run on the direct exact scan.  Synchronous (reads the flag).
+int search_screened(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+                    hipStream_t s) {
+  // candidates: k + 3 while that fits the 8-entry scan lists (k <= 5), else k + 8
+  const int kc = (int)std::min<int64_t>(k + 3 <= 8 ? 8 : k + 8, ix->n);
+  int rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
+  if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
+  if (!rc) rc = ix->flag.ensure(sizeof(int));
+  if (!rc) rc = scan_topk(ix, SCAN_X6, q, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+                     ix->coarse_i.as<int64_t>(), kc, k, os, oi);
+  MQ_HIP(hipGetLastError());
+  if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
+  MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q, ix->dim,
+                     ix->coarse_s.as<float>(), kc, os, k, nq, ix->flag.as<int>());
+  MQ_HIP(hipGetLastError());
+  int bad = 0;
+  MQ_HIP(hipMemcpyAsync(&bad, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  if (!bad) return MQ_OK;
+  ++ix->screen_fallbacks;
+  return scan_topk(ix, SCAN_F32, q, nq, k, os, oi, s);
+}
+
 // Search with queries and outputs already in device memory (asynchronous for k <= 16).
 int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                   hipStream_t s) {
@@ -817,6 +874,8 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
+  if (ix->precision == MQ_DTYPE_F32_SCREEN && nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024)
+    return search_screened(ix, q, nq, k, os, oi, s);
   return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
 }
 
@@ -1052,9 +1111,9 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
 int mq_index_set_precision(mq_index* ix, int dtype) {
   clear_error();
   MQ_CHECK_ARG(ix, "NULL index");
-  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6 || dtype == MQ_DTYPE_BF16,
-               "search precision must be MQ_DTYPE_F32, MQ_DTYPE_F32X6 or MQ_DTYPE_BF16 (got %d)",
-               dtype);
+  MQ_CHECK_ARG(dtype == MQ_DTYPE_F32 || dtype == MQ_DTYPE_F32X6 || dtype == MQ_DTYPE_BF16 ||
+                   dtype == MQ_DTYPE_F32_SCREEN,
+               "search precision must be MQ_DTYPE_F32, _F32X6, _BF16 or _F32_SCREEN (got %d)", dtype);
   MQ_CHECK_ARG(dtype != MQ_DTYPE_BF16 || ix->dim % 64 == 0, "bf16 coarse scan needs dim %% 64 == 0");
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->precision = dtype;
@@ -1068,6 +1127,13 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries) {
                max_queries);
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->stream_max_q = max_queries;
+  return MQ_OK;
+}
+
+int mq_index_screen_fallbacks(const mq_index* ix, int64_t* n) {
+  clear_error();
+  MQ_CHECK_ARG(ix && n, "NULL argument");
+  *n = ix->screen_fallbacks;
   return MQ_OK;
 }
 

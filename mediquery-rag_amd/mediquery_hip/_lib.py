@@ -15,7 +15,7 @@ except Exception:  # pragma: no cover - torch is optional for host-only use
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmqhip.so")
 
 MQ_OK = 0
-MQ_DTYPE_F32, MQ_DTYPE_BF16, MQ_DTYPE_F32X6 = 0, 1, 2
+MQ_DTYPE_F32, MQ_DTYPE_BF16, MQ_DTYPE_F32X6, MQ_DTYPE_F32_SCREEN = 0, 1, 2, 3
 MQ_GELU_ERF, MQ_GELU_TANH = 0, 1
 MQ_POOL_CLS, MQ_POOL_MEAN = 0, 1
 MQ_MAX_K = 64
@@ -64,6 +64,7 @@ SIGNATURES = {
     "mq_index_set_precision": (_I, [_P, _I]),
     "mq_index_set_stream_threshold": (_I, [_P, _I]),
     "mq_index_rescans": (_I, [_P, _P, _P]),
+    "mq_index_screen_fallbacks": (_I, [_P, _P]),
     "mq_index_set_timing": (_I, [_P, _I]),
     "mq_index_read_timing": (_I, [_P, _P, _I]),
     "mq_index_save": (_I, [_P, ctypes.c_char_p]),

@@ -292,3 +292,34 @@ def test_select_gathers_and_compacts(require_gpu):
     assert len(ix) == 0
     with pytest.raises(_lib.MQError, match="out of range"):
         sub.select([6])
+
+
+@pytest.mark.parametrize("k", [1, 5, 50])
+def test_screened_exact_matches_direct_exact(require_gpu, golden, k):
+    """MQ_DTYPE_F32_SCREEN returns the exact fp32 top-k (split-f32 screen + fp32 re-rank,
+    certified): same ids as the direct exact scan outside tie groups, oracle parity."""
+    f = np.load(os.path.join(golden, "flat_golden.npz"))
+    c = synth.corpus(int(f["n"]), int(f["dim"]), clustered=True)
+    q, planted = synth.queries(256, c)
+    ref = exact_scores(q, c)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, k)
+    assert check_topk(i, s, ref, k) == []
+    assert ix.screen_fallbacks == 0
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    s2, i2 = ix.search(q, k)
+    assert check_topk(i2, s2, ref, k) == []
+    np.testing.assert_allclose(s, s2, atol=1e-5)  # two fp32 dot orders
+
+
+def test_screened_falls_back_when_uncertified(require_gpu):
+    """Twenty copies of the best row: the last candidate ties the k-th result, the
+    certificate cannot hold, and the batch is re-run on the direct exact scan."""
+    c = synth.corpus(4000, 768, clustered=True)
+    q, _ = synth.queries(128, c)
+    c[1000:1020] = q[0]  # exact duplicates of query 0's direction
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    assert ix.screen_fallbacks == 1
+    assert i[0].tolist() == [1000, 1001, 1002, 1003, 1004]
+    assert check_topk(i, s, exact_scores(q, c), 5) == []
