@@ -87,6 +87,8 @@ class HipChroma(VectorStoreBase):
         if self._index is None:
             self._dim = dim
             self._index = FlatIndex(dim=dim, device=self._device)
+            # exact fp32 top-k; batched searches run the certified split-f32 screen
+            self._index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
         elif dim != self._dim:
             raise ValueError("embedding dim %d != collection dim %d" % (dim, self._dim))
 
