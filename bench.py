@@ -298,7 +298,7 @@ def main():
                        "hbm_gbs_algorithmic": round(srch_bytes / (sk * 1e-3) / 1e9, 1),
                        "hbm_frac": round(srch_bytes / (sk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        "bytes_per_launch": srch_bytes, "flops_per_launch": flops["flat_search_kernel"],
-                       "traffic": None if scan_x6 else traffic_db.get("flat_search_kernel")}
+                       "traffic": traffic_db.get("flat_search_kernel_x6" if scan_x6 else "flat_search_kernel")}
         return {"value": round(nq_all * args.steps / r["elapsed"], 2),
                 "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
                 "roofline": roof, "search_roofline": search_roof,
