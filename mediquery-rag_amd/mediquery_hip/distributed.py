@@ -74,3 +74,19 @@ class ShardedSearcher:
         allq = self.gather_queries(q_local)
         B = q_local.shape[0]
         return self.search(allq, k, keep=(rank * B, (rank + 1) * B))  # merge own rows only
+
+
+def ingest_sharded(texts, embed_fn, index_add, world=None, rank=None, group=None, chunk=4096):
+    """Data-parallel ingest (the reference's `Chroma.from_documents` at
+    src/ingest_medical.py:106-110 embeds every chunk on one Ollama server).  Rank r
+    embeds only its contiguous block `shard_bounds(len(texts), world, r)` with
+    `embed_fn(texts) -> [n, dim]` and appends it to its local shard with
+    `index_add(rows)`, `chunk` texts at a time.  No collective: the block layout is the
+    one `ShardedSearcher` assumes (global id = offset + local id), so the returned
+    offset is that searcher's `offset`.  -> (offset, count)."""
+    world = dist.get_world_size(group) if world is None else world
+    rank = dist.get_rank(group) if rank is None else rank
+    off, cnt = shard_bounds(len(texts), world, rank)
+    for s in range(off, off + cnt, chunk):
+        index_add(embed_fn(texts[s:min(s + chunk, off + cnt)]))
+    return off, cnt

@@ -84,3 +84,28 @@ def test_sharded_search_equals_single_index(world, N, K):
         np.testing.assert_array_equal(ids_dp, ids[rank * half:(rank + 1) * half])
     for r in res[1:]:
         np.testing.assert_array_equal(res[0][1], r[1])
+
+
+@pytest.mark.parametrize("world,N,chunk", [(2, 997, 64), (3, 10, 4), (4, 3, 8)])
+def test_ingest_sharded_blocks_line_up_with_search_ids(world, N, chunk):
+    """Each rank's `ingest_sharded` block, appended in order, must be exactly rows
+    [offset, offset+count) of the single-process ingest, so local id + offset is the
+    global row id `ShardedSearcher` reports."""
+    from mediquery_hip.distributed import ingest_sharded
+    texts = ["doc %d" % i for i in range(N)]
+
+    def embed(ts):  # deterministic stand-in for the encoder: one row per text
+        return np.array([[float(t.split()[1]), len(t)] for t in ts], np.float32).reshape(-1, 2)
+
+    whole = embed(texts)
+    seen = []
+    for rank in range(world):
+        rows = []
+        off, cnt = ingest_sharded(texts, embed, rows.append, world=world, rank=rank, chunk=chunk)
+        local = np.concatenate(rows) if rows else np.zeros((0, 2), np.float32)
+        assert local.shape[0] == cnt
+        assert all(r.shape[0] <= chunk for r in rows)
+        np.testing.assert_array_equal(local, whole[off:off + cnt])
+        seen.append((off, cnt))
+    assert seen[0][0] == 0 and sum(c for _, c in seen) == N
+    assert all(seen[r][0] + seen[r][1] == seen[r + 1][0] for r in range(world - 1))
