@@ -36,9 +36,10 @@ from mediquery_hip.native import Encoder, FlatIndex  # noqa: E402
 from mediquery_hip import _lib  # noqa: E402
 
 # run name -> (encoder arithmetic, search mode).  The headline "f32" computes exact fp32
-# results: the encoder on the f32 MFMA, the top-k by the certified screen (split-f32 scan
-# for k+3 candidates, fp32 re-rank, proven bound, direct exact scan on failure).  The same
-# run times the direct exact scan ("f32_direct_search") and the all-split-f32 variant.
+# results: the encoder on the f32 MFMA, the top-k by certified screens (bf16-shadow scan
+# for 64 candidates, fp32 re-rank, proven bound per query; uncertified queries re-run on
+# the split-f32 screen or the direct exact scan).  The same run times the direct exact
+# scan ("f32_direct_search") and the all-split-f32 variant.
 PRECISIONS = {"f32": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32_SCREEN),
               "f32_direct_search": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32),
               "f32x6": (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32X6)}
@@ -59,6 +60,8 @@ def parse():
     p.add_argument("--k", type=int, default=5)
     p.add_argument("--layers", type=int, default=DMETA_BASE.layers)
     p.add_argument("--single-iters", type=int, default=50, help="single-query latency samples")
+    p.add_argument("--secondary-seq-len", type=int, default=128,
+                   help="also time the headline step at this L (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     return p.parse_args()
@@ -165,7 +168,7 @@ def main():
         max over ranks); per-kernel-class device time from HIP events."""
         enc.set_precision(precs[0])
         index.set_precision(precs[1])
-        fb0 = index.screen_fallbacks
+        fb0, pd0 = index.screen_fallbacks, index.screen_passdowns
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         for _ in range(args.warmup):
             step()
@@ -194,6 +197,7 @@ def main():
         enc.set_timing(False)
         index.set_timing(False)
         return {"elapsed": elapsed, "stage_ms": stage_ms, "screen_fallbacks": index.screen_fallbacks - fb0,
+                "screen_passdowns": index.screen_passdowns - pd0,
                 "enc_ms": statistics.mean(e[0].elapsed_time(e[1]) for e in evs),
                 "srch_ms": statistics.mean(e[1].elapsed_time(e[2]) for e in evs)}
 
@@ -228,6 +232,25 @@ def main():
                 "recall_at_k_vs_exact_f32": round(hits / (B * k5), 5),
                 "hbm_gbs_algorithmic": round(cnt * 768 * 2 / (ms5 * 1e-3) / 1e9, 1)}
         index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+
+    # ---- SURVEY.md §8d secondary run: the same step at L = 128 (headline arithmetic) ----
+    sec = None
+    if world == 1 and args.secondary_seq_len > 0:
+        L2 = args.secondary_seq_len
+        ids2_np, mask2_np = synth.token_batch(B, L2, seed=synth.TOKEN_SEED)
+        ids2, mask2 = torch.from_numpy(ids2_np).to(dev), torch.from_numpy(mask2_np).to(dev)
+        n2 = max(3, args.steps // 4)
+        for it in range(2 + n2):
+            if it == 2:
+                torch.cuda.synchronize()
+                a = time.perf_counter()
+            enc.embed_device(ids2, mask2, q)
+            local_search(q, K)
+        torch.cuda.synchronize()
+        t2 = (time.perf_counter() - a) / n2
+        sec = {"seq_len": L2, "steps": n2, "queries_per_s": round(B / t2, 1),
+               "ms_per_step": round(t2 * 1e3, 3),
+               "encoder_tflops_effective": round(encoder_flops(cfg, B, L2) / t2 / 1e12, 2)}
 
     # ---- single-query latency (embed 1 query + search the shard), exact f32 ----------
     lat = []
@@ -272,39 +295,44 @@ def main():
 
     def summarize(name, r):
         enc_x6 = PRECISIONS[name][0] == _lib.MQ_DTYPE_F32X6
-        scan_x6 = PRECISIONS[name][1] in (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32_SCREEN)
+        # arithmetic of the timed scan kernel: the screen's first tier scans the bf16 shadow
+        scan = {_lib.MQ_DTYPE_F32X6: "x6", _lib.MQ_DTYPE_F32_SCREEN: "bf16"}.get(PRECISIONS[name][1], "f32")
+        scan_peak = {"x6": X6_PEAK, "bf16": BF16_PEAK_TFLOPS, "f32": FP32_PEAK_TFLOPS}[scan]
         kernels = {}
         for kname, ms in r["stage_ms"].items():
             d = {"ms_per_step": round(ms, 4)}
             if kname in flops and ms > 0:
-                pk = (scan_x6 if kname == "flat_search_kernel" else enc_x6) and X6_PEAK or FP32_PEAK_TFLOPS
+                pk = scan_peak if kname == "flat_search_kernel" else (X6_PEAK if enc_x6 else FP32_PEAK_TFLOPS)
                 tf = flops[kname] / (ms * 1e-3) / 1e12
                 d.update(tflops=round(tf, 2), frac_peak=round(tf / pk, 4))
             kernels[kname] = d
         dom = max((n for n in flops if r["stage_ms"].get(n, 0) > 0), key=lambda n: r["stage_ms"][n])
-        dom_x6 = scan_x6 if dom == "flat_search_kernel" else enc_x6
-        peak = X6_PEAK if dom_x6 else FP32_PEAK_TFLOPS
+        dom_x6 = (scan == "x6") if dom == "flat_search_kernel" else enc_x6
+        peak = (scan_peak if dom == "flat_search_kernel" else X6_PEAK if enc_x6 else FP32_PEAK_TFLOPS)
         dom_tf = flops[dom] / (r["stage_ms"][dom] * 1e-3) / 1e12
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(dom_tf, 2), "peak": round(peak, 1),
                 "unit": "TFLOP/s (fp32-equivalent)" if dom_x6 else "TFLOP/s",
                 "frac": round(dom_tf / peak, 4),
                 "traffic": None if dom_x6 else traffic_db.get(dom)}
         sk = r["stage_ms"].get("flat_search_kernel", r["srch_ms"])
-        speak = X6_PEAK if scan_x6 else FP32_PEAK_TFLOPS
-        search_roof = {"kernel": "flat_search_kernel (%s)" % ("split-f32" if scan_x6 else "exact f32"),
-                       "bound": "mfma",
+        # bf16 scan: 1.5 GB of shadow rows, intensity 256 FLOP/B < the bf16 ridge -> HBM-bound
+        sbytes = srch_bytes if scan != "bf16" else cnt * 768 * 2 + nq_all * 768 * 2 + nq_all * K * 8
+        search_roof = {"kernel": "flat_search_kernel (%s)" % {"x6": "split-f32", "bf16": "bf16 screen",
+                                                               "f32": "exact f32"}[scan],
+                       "bound": "hbm" if scan == "bf16" else "mfma",
                        "achieved_tflops": kernels.get("flat_search_kernel", {}).get("tflops"),
-                       "peak": round(speak, 1),
-                       "hbm_gbs_algorithmic": round(srch_bytes / (sk * 1e-3) / 1e9, 1),
-                       "hbm_frac": round(srch_bytes / (sk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                       "bytes_per_launch": srch_bytes, "flops_per_launch": flops["flat_search_kernel"],
-                       "traffic": traffic_db.get("flat_search_kernel_x6" if scan_x6 else "flat_search_kernel")}
+                       "peak_tflops": round(scan_peak, 1),
+                       "hbm_gbs_algorithmic": round(sbytes / (sk * 1e-3) / 1e9, 1),
+                       "hbm_frac": round(sbytes / (sk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "bytes_per_launch": sbytes, "flops_per_launch": flops["flat_search_kernel"],
+                       "traffic": traffic_db.get({"x6": "flat_search_kernel_x6", "bf16": "flat_search_kernel_bf16",
+                                                  "f32": "flat_search_kernel"}[scan])}
         return {"value": round(nq_all * args.steps / r["elapsed"], 2),
                 "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
                 "roofline": roof, "search_roofline": search_roof,
                 "encoder_ms": round(r["enc_ms"], 3), "search_ms": round(r["srch_ms"], 3),
                 "kernels": kernels, "planted_top1_ok": ok_planted[name],
-                "screen_fallbacks": r["screen_fallbacks"]}
+                "screen_fallbacks": r["screen_fallbacks"], "screen_passdowns": r["screen_passdowns"]}
 
     main_r = summarize("f32", runs["f32"])
     direct_r = summarize("f32_direct_search", runs["f32_direct_search"])
@@ -327,15 +355,17 @@ def main():
         "search_roofline": main_r["search_roofline"],
         "encoder_ms": main_r["encoder_ms"], "search_ms": main_r["search_ms"],
         "kernels": main_r["kernels"],
-        "search_mode": "exact fp32 top-k: split-f32 screen for k+3 candidates, fp32 re-rank, "
-                       "certified bound (direct exact scan when it fails; %d fallbacks in the timed "
-                       "steps)" % main_r["screen_fallbacks"],
+        "search_mode": "exact fp32 top-k: bf16-shadow MFMA screen for 64 candidates, fp32 re-rank, "
+                       "certified bound per query; uncertified queries re-run on the split-f32 screen "
+                       "(%d in the timed steps) or the direct exact scan (%d)"
+                       % (main_r["screen_passdowns"], main_r["screen_fallbacks"]),
         "f32_direct_search": {kk: direct_r[kk] for kk in ("value", "ms_per_step", "search_ms",
                                                           "search_roofline", "planted_top1_ok")},
         "split_f32": dict(alt_r, dtype="f32 via exact 3-way bf16 split (6 bf16 MFMAs / product, "
                                        "fp32 accumulate); same parity tolerances as f32"),
     }
     out["config5_bf16_rerank"] = cfg5
+    out["secondary_long_queries"] = sec
     if world == 1 and not args.no_cpu_baseline:
         def corpus_host():
             return torch.nn.functional.normalize(

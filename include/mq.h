@@ -46,9 +46,10 @@ extern "C" {
 #define MQ_DTYPE_BF16 1   /* bf16 storage (coarse paths)                                    */
 #define MQ_DTYPE_F32X6 2  /* fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMAs per
                            * product, fp32 accumulate: fp32-class error, 2.67x the MFMA rate */
-#define MQ_DTYPE_F32_SCREEN 3 /* search only: exact fp32 top-k at the F32X6 rate - split-f32
-                               * scan for k + 3..8 candidates, fp32 re-rank, certified bound
-                               * (else the direct exact scan); batches > 64, k <= 56 */
+#define MQ_DTYPE_F32_SCREEN 3 /* search only: exact fp32 top-k through certified screens -
+                               * bf16 shadow scan for k + 8..16 candidates, fp32 re-rank,
+                               * proven error bound; uncertified queries re-run on the
+                               * split-f32 screen, then the direct exact scan */
 
 #define MQ_GELU_ERF 0  /* exact erf GELU (HF BERT "gelu")            */
 #define MQ_GELU_TANH 1 /* tanh approximation (ggml / llama.cpp gelu)  */
@@ -100,8 +101,9 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
  * MQ_DTYPE_BF16: bf16 shadow slab scanned on bf16 MFMA for the top max(k, 50) (capped
  * at MQ_MAX_K) candidates, then an exact fp32 re-rank to the top-k (BASELINE config 5;
  * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0.
- * MQ_DTYPE_F32_SCREEN: exact fp32 results via the certified split-f32 screen (above);
- * scores are the fp32 re-rank's dot products. */
+ * MQ_DTYPE_F32_SCREEN: exact fp32 results via certified screens (above): single queries
+ * stream the bf16 shadow (half the HBM bytes), batches scan it on bf16 MFMA; scores are
+ * the fp32 re-rank's dot products.  Synchronous (reads the certificate count back). */
 int mq_index_set_precision(mq_index* ix, int dtype);
 /* Batches of at most `max_queries` queries (default 4, 0..16; dim % 64 == 0, dim <= 1024)
  * use the streaming fp32 kernel instead of the MFMA tiles, whatever the precision. */
@@ -109,9 +111,10 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries);
 /* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
  * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
-/* Screened searches (MQ_DTYPE_F32_SCREEN) whose certificate failed and that were re-run
- * on the direct exact scan. */
-int mq_index_screen_fallbacks(const mq_index* ix, int64_t* n);
+/* Screen counters (MQ_DTYPE_F32_SCREEN; either pointer may be NULL): queries whose
+ * certificates failed and that were re-run on the direct exact scan, and bf16-screened
+ * queries re-run on the split-f32 screen. */
+int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
 /* Device-time accounting with HIP events on the launch stream (off by default).

@@ -204,9 +204,12 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
 // lane group, fp32 FMA, a 16-lane butterfly per (row, query), and lane j of the group
 // keeps query j's register top list; the block merges its 16 groups' lists at the end.
 // List = block: cand[block][query][0..kl).
-constexpr int kStreamMaxNV = 16;  // float4 per lane per row: dim <= 1024
+// BF: the rows are the bf16 shadow (half the bytes; a 16-B load carries 8 elements, each
+// widened exactly to fp32 and multiplied with the fp32 query) - the certified screen's
+// single-query scan.
+constexpr int kStreamMaxNV = 16;  // 16-B loads per lane per row: dim <= 1024
 
-template <int NQ, int KC, int NV>
+template <int NQ, int KC, int NV, bool BF = false>
 __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restrict__ Q, int nq,
                                                             const float* __restrict__ C,
                                                             int64_t n_rows, int dim, int kl,
@@ -219,13 +222,16 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
     qs[i] = j < nq ? Q[(int64_t)j * dim + (i - j * dim)] : 0.f;
   }
   __syncthreads();
-  const int nv = NV == kStreamMaxNV ? dim >> 6 : NV;  // NV < max: compiled for dim = 64 NV
+  constexpr int EPV = BF ? 8 : 4;  // elements per 16-B load
+  // NV < max: compiled for dim = 16 EPV NV
+  const int nv = NV == kStreamMaxNV ? dim / (16 * EPV) : NV;
+  const int row_words = BF ? dim / 2 : dim;  // row stride in 4-byte words
   const int64_t group = (int64_t)blockIdx.x * 16 + (tid >> 4);
   const int64_t n_groups = (int64_t)gridDim.x * 16;
   TopList<KC> top;
   top.init();
   const bool owner = gl < nq && gl < NQ;  // lane gl keeps query gl's list
-  const float* qbase = qs + gl * 4;
+  const float* qbase = qs + gl * EPV;
 
   auto score_rows = [&](const floatx4 (&v)[2][NV], int64_t r0, int nr)
       __attribute__((always_inline)) {
@@ -242,9 +248,20 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
 #pragma unroll
         for (int it = 0; it < NV; ++it) {
           if (it < nv) {
-            const floatx4 qv = *reinterpret_cast<const floatx4*>(qj + it * 64);
-            acc = fmaf(v[u][it].x, qv.x, fmaf(v[u][it].y, qv.y,
-                  fmaf(v[u][it].z, qv.z, fmaf(v[u][it].w, qv.w, acc))));
+            if constexpr (BF) {
+              const floatx4 q0 = *reinterpret_cast<const floatx4*>(qj + it * 128);
+              const floatx4 q1 = *reinterpret_cast<const floatx4*>(qj + it * 128 + 4);
+              const unsigned w0 = __float_as_uint(v[u][it].x), w1 = __float_as_uint(v[u][it].y);
+              const unsigned w2 = __float_as_uint(v[u][it].z), w3 = __float_as_uint(v[u][it].w);
+              acc = fmaf(bf16_lo(w0), q0.x, fmaf(bf16_hi(w0), q0.y,
+                    fmaf(bf16_lo(w1), q0.z, fmaf(bf16_hi(w1), q0.w, acc))));
+              acc = fmaf(bf16_lo(w2), q1.x, fmaf(bf16_hi(w2), q1.y,
+                    fmaf(bf16_lo(w3), q1.z, fmaf(bf16_hi(w3), q1.w, acc))));
+            } else {
+              const floatx4 qv = *reinterpret_cast<const floatx4*>(qj + it * 64);
+              acc = fmaf(v[u][it].x, qv.x, fmaf(v[u][it].y, qv.y,
+                    fmaf(v[u][it].z, qv.z, fmaf(v[u][it].w, qv.w, acc))));
+            }
           }
         }
 #pragma unroll
@@ -262,7 +279,7 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const floatx4* rp =
-          reinterpret_cast<const floatx4*>(C + (u < nr ? r0 + u * n_groups : r0) * dim) + gl;
+          reinterpret_cast<const floatx4*>(C + (u < nr ? r0 + u * n_groups : r0) * row_words) + gl;
 #pragma unroll
       for (int it = 0; it < NV; ++it)
         if (it < nv) v[u][it] = __builtin_nontemporal_load(rp + it * 16);
@@ -330,6 +347,52 @@ __global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ 
   dst[i] = pk_bf16(v.x, v.y);
 }
 
+// bf16 shadow of stored rows (same layout as to_bf16_kernel) plus the rounding
+// statistics the certified screens need: max over rows of ||c - bf16(c)|| into stats[0]
+// and of ||c|| into stats[1] (non-negative floats order like their bit patterns, so an
+// unsigned atomicMax is a float max).  One wave per row.
+__global__ __launch_bounds__(256) void bf16_shadow_kernel(const float* __restrict__ src,
+                                                          unsigned* __restrict__ dst, int64_t n,
+                                                          int dim, unsigned* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const floatx4* s = reinterpret_cast<const floatx4*>(src + row * dim);
+  uint2* d = reinterpret_cast<uint2*>(dst + row * (dim / 2));
+  float sd = 0.f, sc = 0.f;
+  for (int i = lane; i < (dim >> 2); i += 64) {
+    const floatx4 v = s[i];
+    const unsigned a = pk_bf16(v.x, v.y), b = pk_bf16(v.z, v.w);
+    d[i] = make_uint2(a, b);
+    const float e0 = v.x - bf16_lo(a), e1 = v.y - bf16_hi(a);  // exact residuals
+    const float e2 = v.z - bf16_lo(b), e3 = v.w - bf16_hi(b);
+    sd += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+    sc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sd += __shfl_xor(sd, off);
+    sc += __shfl_xor(sc, off);
+  }
+  if (lane == 0) {
+    atomicMax(stats, __float_as_uint(sqrtf(sd)));
+    atomicMax(stats + 1, __float_as_uint(sqrtf(sc)));
+  }
+}
+
+// Results of a re-run subset back into the caller's [nq, k] outputs: row j -> idx[j].
+__global__ __launch_bounds__(256) void scatter_results_kernel(const float* __restrict__ ss,
+                                                              const int64_t* __restrict__ si,
+                                                              const int64_t* __restrict__ idx,
+                                                              int64_t n, int k, float* __restrict__ os,
+                                                              int64_t* __restrict__ oi) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * k) return;
+  const int64_t j = t / k, c = t - j * k;
+  os[idx[j] * k + c] = ss[t];
+  oi[idx[j] * k + c] = si[t];
+}
+
 // Exact fp32 re-rank of the coarse candidates: one block per query, one wave per
 // candidate dot product (768-wide, float4 per lane), then every candidate's rank by
 // (score desc, id asc) picks its output slot.
@@ -343,21 +406,33 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  for (int c = wave; c < kc; c += 4) {
-    const long long id = cand[q * kc + c];
-    float acc = 0.f;
-    if (id >= 0) {
-      const floatx4* r4 = reinterpret_cast<const floatx4*>(rows + id * dim);
-      for (int i = lane; i < dim / 4; i += 64) {
-        const floatx4 a = q4[i], b = r4[i];
-        acc = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc))));
-      }
+  // four candidates per wave per round, their row loads in flight together
+  for (int c0 = wave * 4; c0 < kc; c0 += 16) {
+    long long id[4];
+    float acc[4];
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    for (int u = 0; u < 4; ++u) {
+      id[u] = c0 + u < kc ? cand[q * kc + c0 + u] : -1;
+      acc[u] = 0.f;
     }
-    if (lane == 0) {
-      sc[c] = id >= 0 ? acc : -INFINITY;
-      sid[c] = id;
+    for (int i = lane; i < dim / 4; i += 64) {
+      const floatx4 a = q4[i];
+      floatx4 b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        b[u] = id[u] >= 0 ? reinterpret_cast<const floatx4*>(rows + id[u] * dim)[i] : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
+      if (lane == 0 && c0 + u < kc) {
+        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
+        sid[c0 + u] = id[u];
+      }
     }
   }
   __syncthreads();
@@ -374,31 +449,66 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
-// Certificate of the screened exact search (MQ_DTYPE_F32_SCREEN).  The split-f32 scan
-// kept the kc best candidates of each query by its score s; a row r outside them has
-// s_r <= s_kc.  Every split-f32 score is within eps of the exact dot (dropped split
-// terms < 3 2^-24 |q||c| per product, fp32 accumulation over <= 64 x 6 MFMA steps:
-// <= 2.5e-5 ||q|| for unit rows and dim <= 1024) and so is every fp32 re-rank score
-// (<= 18 roundings), eps = 4e-5 ||q||.  Hence s_kc + 2 eps < e_k (the re-ranked k-th
-// score) proves no outside row can enter the exact top-k; otherwise flag the batch for
-// the direct exact scan.  One wave per query.
+// Certificate of the screened exact search (MQ_DTYPE_F32_SCREEN).  A screen scan kept
+// the kc best rows of each query by its approximate score s, so a row r outside them
+// has s_r <= s_kc; if every s is within E of the exact dot e, and e_k (the fp32 re-rank
+// of the candidates, k-th best) is within its own rounding bound, then
+// s_kc + E_total < e_k proves no outside row can enter the exact top-k.  E per mode:
+//  VERIFY_X6 (split-f32 MFMA scan): dropped split terms < 3 2^-24 |q||c| per product,
+//    fp32 accumulation over <= 64 x 6 MFMA steps: <= 2.5e-5 ||q|| for unit rows and
+//    dim <= 1024; re-rank <= 18 roundings; E_total = 2 x 4e-5 ||q||.
+//  VERIFY_BF16_Q16 (bf16 MFMA scan, query rounded to bf16 bq, row to bc):
+//    |q.c - bq.bc| <= ||q - bq|| ||c|| + ||bq|| ||c - bc|| (Cauchy-Schwarz), fp32
+//    accumulation <= g ||bq|| ||bc|| with g = 2 dim 2^-24, re-rank <= g ||q|| ||c||;
+//    ||c|| <= cmax and ||c - bc|| <= dmax are the shadow's measured maxima (stats).
+//  VERIFY_BF16_Q32 (bf16 rows streamed against the fp32 query): as above, ||q - bq|| = 0.
+// A query that fails is appended to fail[] (count in *n_fail) and re-run one tier down.
+// One wave per query.
+enum { VERIFY_X6 = 0, VERIFY_BF16_Q16 = 1, VERIFY_BF16_Q32 = 2 };
+
 __global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restrict__ Q, int dim,
                                                             const float* __restrict__ cs, int kc,
                                                             const float* __restrict__ es, int k,
-                                                            int64_t nq, int* __restrict__ flag) {
+                                                            int64_t nq, int mode,
+                                                            const unsigned* __restrict__ stats,
+                                                            int* __restrict__ n_fail,
+                                                            int64_t* __restrict__ fail) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  float ss = 0.f;
+  float ss = 0.f, sd = 0.f, sb = 0.f;
   for (int i = lane; i < (dim >> 2); i += 64) {
     const floatx4 v = q4[i];
     ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    if (mode == VERIFY_BF16_Q16) {  // the same rounding as to_bf16_kernel
+      const unsigned a = pk_bf16(v.x, v.y), b = pk_bf16(v.z, v.w);
+      const float b0 = bf16_lo(a), b1 = bf16_hi(a), b2 = bf16_lo(b), b3 = bf16_hi(b);
+      const float e0 = v.x - b0, e1 = v.y - b1, e2 = v.z - b2, e3 = v.w - b3;
+      sd += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+      sb += b0 * b0 + b1 * b1 + b2 * b2 + b3 * b3;
+    }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-  const float eps = 4e-5f * sqrtf(ss);
-  if (lane == 0 && !(cs[q * kc + kc - 1] + 2.f * eps < es[q * k + k - 1])) atomicOr(flag, 1);
+  for (int off = 32; off > 0; off >>= 1) {
+    ss += __shfl_xor(ss, off);
+    sd += __shfl_xor(sd, off);
+    sb += __shfl_xor(sb, off);
+  }
+  if (lane != 0) return;
+  const float qn = sqrtf(ss);
+  float E;
+  if (mode == VERIFY_X6) {
+    E = 8e-5f * qn;
+  } else {
+    // 1.001: slack for the fp32 evaluation of the norms and of this bound
+    const float dmax = __uint_as_float(stats[0]) * 1.001f, cmax = __uint_as_float(stats[1]) * 1.001f;
+    const float g = 2.f * (float)dim * 5.9604645e-8f;
+    const float dq = mode == VERIFY_BF16_Q16 ? sqrtf(sd) : 0.f;
+    const float bqn = mode == VERIFY_BF16_Q16 ? sqrtf(sb) : qn;
+    E = (dq * cmax + bqn * dmax + g * bqn * (cmax + dmax) + g * qn * cmax) * 1.001f + 1e-7f;
+  }
+  if (!(cs[q * kc + kc - 1] + E < es[q * k + k - 1])) fail[atomicAdd(n_fail, 1)] = q;
 }
 
 // ======================================================= K10: merge lists ======
@@ -605,11 +715,14 @@ struct mq_index {
   DevBuf stage, cand_s, cand_i, out_s, out_i;
   DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
   int64_t n16 = 0;   // rows already mirrored into rows16
+  DevBuf stats16;    // shadow rounding maxima: [0] max ||c - bf16(c)||, [1] max ||c|| (float bits)
   DevBuf q16, coarse_s, coarse_i;
-  DevBuf flag;          // merge overflow flag (k > 16)
+  DevBuf flag;          // merge overflow flag (k > 16) / screen failure count
+  DevBuf tier_fail[3], tier_q[3], tier_s[3], tier_i[3];  // per screen tier: re-run subset
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
   int64_t remerges = 0;  // merges re-run with 64-entry thread lists
-  int64_t screen_fallbacks = 0;  // screened searches whose certificate failed
+  int64_t screen_fallbacks = 0;  // screened queries re-run on the direct exact scan
+  int64_t screen_passdowns = 0;  // bf16-screened queries re-run on the split-f32 screen
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
@@ -681,9 +794,9 @@ int fill_padding(float* os, int64_t* oi, int64_t count, hipStream_t s) {
   return MQ_OK;
 }
 
-enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16, SCAN_STREAM };
+enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16, SCAN_STREAM, SCAN_STREAM16 };
 
-template <int NQ, int KC>
+template <int NQ, int KC, bool BF>
 void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
                       int* ci, hipStream_t s) {
   // query image, then the block merge's [16][NQ][KC] (score, id) lists in the same LDS
@@ -692,28 +805,28 @@ void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int bl
     if (lds > 64 * 1024)  // above the default dynamic-LDS limit (64-entry lists, NQ >= 8)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, q, nq, ix->rows, ix->n, ix->dim, kl, cs,
-                       ci);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, q, nq,
+                       BF ? ix->rows16.as<float>() : ix->rows, ix->n, ix->dim, kl, cs, ci);
   };
   if (ix->dim == 768)  // the dmeta / BERT-base width, register arrays sized exactly
-    launch(stream_search_kernel<NQ, KC, 12>);
+    launch(stream_search_kernel<NQ, KC, BF ? 6 : 12, BF>);
   else
-    launch(stream_search_kernel<NQ, KC, kStreamMaxNV>);
+    launch(stream_search_kernel<NQ, KC, kStreamMaxNV, BF>);
 }
 
-template <int KC>
+template <int KC, bool BF = false>
 void launch_stream(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
                    int* ci, hipStream_t s) {
   if (nq <= 1)
-    launch_stream_nq<1, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<1, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
   else if (nq <= 2)
-    launch_stream_nq<2, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<2, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
   else if (nq <= 4)
-    launch_stream_nq<4, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<4, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
   else if (nq <= 8)
-    launch_stream_nq<8, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<8, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
   else
-    launch_stream_nq<16, KC>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<16, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
 }
 
 // streaming-kernel grid: up to 2 blocks per CU, at least ~8 rows per lane group
@@ -755,7 +868,8 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
     const int kl = std::min(kc, k);
     const bool check = kl < k;
     SearchPlan p = plan_search(ix, nq, kc);
-    if (kind == SCAN_STREAM) p.n_lists = stream_blocks(ix);  // one list per block
+    const bool stream = kind == SCAN_STREAM || kind == SCAN_STREAM16;
+    if (stream) p.n_lists = stream_blocks(ix);  // one list per block
     const size_t n_cand = (size_t)p.n_lists * nq * kl;
     int rc = ix->cand_s.ensure(n_cand * sizeof(float));
     if (!rc) rc = ix->cand_i.ensure(n_cand * sizeof(int));
@@ -773,6 +887,13 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
         case 8: launch_stream<8>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
         case 16: launch_stream<16>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
         default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+      }
+    } else if (kind == SCAN_STREAM16) {
+      const int nb = stream_blocks(ix);
+      switch (kc) {
+        case 8: launch_stream<8, true>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+        case 16: launch_stream<16, true>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+        default: launch_stream<MQ_MAX_K, true>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
       }
     } else switch (kc) {
       case 8: launch_scan<8>(ix, kind, p.wide, q, (int)nq, kl, p.G, p.nqt, cs, ci, s); break;
@@ -805,25 +926,42 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
   }
 }
 
+// bf16 shadow of the stored rows, mirrored lazily (rows added since the last bf16 search),
+// with the rounding maxima the bf16 screens certify against (reset on a rebuild).
+int ensure_shadow(mq_index* ix, hipStream_t s) {
+  int rc = ix->rows16.ensure((size_t)ix->cap * ix->dim * 2);
+  if (!rc) rc = ix->stats16.ensure(2 * sizeof(unsigned));
+  if (rc) return rc;
+  if (ix->n16 < ix->n) {
+    if (ix->n16 == 0) MQ_HIP(hipMemsetAsync(ix->stats16.p, 0, 2 * sizeof(unsigned), s));
+    const int64_t nr = ix->n - ix->n16;
+    hipLaunchKernelGGL(bf16_shadow_kernel, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, s,
+                       ix->rows + ix->n16 * ix->dim,
+                       ix->rows16.as<unsigned>() + ix->n16 * ix->dim / 2, nr, ix->dim,
+                       ix->stats16.as<unsigned>());
+    MQ_HIP(hipGetLastError());
+    ix->n16 = ix->n;
+  }
+  return MQ_OK;
+}
+
+int queries_to_bf16(mq_index* ix, const float* q, int64_t nq, hipStream_t s) {
+  int rc = ix->q16.ensure((size_t)nq * ix->dim * 2);
+  if (rc) return rc;
+  const int64_t qpairs = nq * ix->dim / 2;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((qpairs + 255) / 256)), dim3(256), 0, s, q,
+                     ix->q16.as<unsigned>(), qpairs);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
 // Config 5: bf16 coarse scan for the best `kc` rows per query (kc = max(2k, 50) capped
 // at MQ_MAX_K and n), then an exact fp32 re-rank of those candidates to the final top-k.
 int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                        hipStream_t s) {
-  const int64_t dim = ix->dim;
-  int rc = ix->rows16.ensure((size_t)ix->cap * dim * 2);
+  int rc = ensure_shadow(ix, s);
+  if (!rc) rc = queries_to_bf16(ix, q, nq, s);
   if (rc) return rc;
-  if (ix->n16 < ix->n) {  // mirror rows added since the last bf16 search
-    const int64_t pairs = (ix->n - ix->n16) * dim / 2;
-    hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s,
-                       ix->rows + ix->n16 * dim, ix->rows16.as<unsigned>() + ix->n16 * dim / 2,
-                       pairs);
-    ix->n16 = ix->n;
-  }
-  rc = ix->q16.ensure((size_t)nq * dim * 2);
-  if (rc) return rc;
-  const int64_t qpairs = nq * dim / 2;
-  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((qpairs + 255) / 256)), dim3(256), 0, s, q,
-                     ix->q16.as<unsigned>(), qpairs);
   const int kc = (int)std::min<int64_t>(std::max(2 * k, 50), std::min<int64_t>(MQ_MAX_K, ix->n));
   rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
   if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
@@ -836,46 +974,109 @@ int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* o
   return MQ_OK;
 }
 
-// Exact fp32 top-k at the split-f32 rate (MQ_DTYPE_F32_SCREEN, batches > 64): the
-// split-f32 scan keeps kc = k + 3..8 candidates per query, an fp32 re-rank orders them, and
-// screen_verify_kernel certifies that no other row can enter the top-k; a batch with
-// any uncertified query is re-run on the direct exact scan.  Synchronous (reads the flag).
-int search_screened(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
-                    hipStream_t s) {
-  // candidates: k + 3 while that fits the 8-entry scan lists (k <= 5), else k + 8
-  const int kc = (int)std::min<int64_t>(k + 3 <= 8 ? 8 : k + 8, ix->n);
-  int rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
+// The direct exact fp32 scan: streaming kernel for a handful of queries, MFMA tiles else.
+bool stream_ok(const mq_index* ix) { return ix->dim % 64 == 0 && ix->dim <= 64 * kStreamMaxNV; }
+
+int search_direct(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+                  hipStream_t s) {
+  if (nq <= ix->stream_max_q && stream_ok(ix)) return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
+  return scan_topk(ix, SCAN_F32, q, nq, k, os, oi, s);
+}
+
+// Exact fp32 top-k through certified screens (MQ_DTYPE_F32_SCREEN).  A tier scans with
+// cheaper arithmetic for kc > k candidates per query, re-ranks them in fp32
+// (rerank_kernel) and certifies each query (screen_verify_kernel); the queries whose
+// certificate fails are gathered and re-run one tier down, and their results scattered
+// back.  Tiers:
+//   TIER_BF16_STREAM  few queries: bf16 shadow streamed against the fp32 query (half the
+//                     HBM bytes of the exact stream) -> direct exact stream
+//   TIER_BF16         batches: bf16 MFMA scan of the shadow -> split-f32 tier (> 64
+//                     failing queries) or the direct exact scan
+//   TIER_X6           split-f32 MFMA scan -> direct exact scan
+// Synchronous (reads the failure count).
+enum ScreenTier { TIER_BF16_STREAM = 0, TIER_BF16 = 1, TIER_X6 = 2 };
+
+bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
+  return nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024;
+}
+
+int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, float* os,
+                    int64_t* oi, hipStream_t s) {
+  const bool bf = tier != TIER_X6;
+  // candidates: the bf16 screen's error bound is ~3.5e-3 for unit vectors, so it keeps
+  // a wide margin - 64 per query in batches (the k-th and 64-th scores of 1M random-ish
+  // rows are ~0.02 apart), max(32, k + 16) for a few streamed queries; the split-f32
+  // screen (bound 8e-5) keeps k + 3 while that fits its 8-entry lists (k <= 5), else k + 8
+  const int want = tier == TIER_BF16 ? MQ_MAX_K
+                   : tier == TIER_BF16_STREAM ? std::min(std::max(32, k + 16), MQ_MAX_K)
+                   : (k + 3 <= 8 ? 8 : k + 8);
+  const int kc = (int)std::min<int64_t>(want, ix->n);
+  int rc = bf ? ensure_shadow(ix, s) : MQ_OK;
+  if (!rc && tier == TIER_BF16) rc = queries_to_bf16(ix, q, nq, s);
+  if (!rc) rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
   if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
   if (!rc) rc = ix->flag.ensure(sizeof(int));
-  if (!rc) rc = scan_topk(ix, SCAN_X6, q, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
+  if (!rc) rc = ix->tier_fail[tier].ensure((size_t)nq * sizeof(int64_t));
+  if (rc) return rc;
+  const int kind = tier == TIER_X6 ? SCAN_X6 : tier == TIER_BF16 ? SCAN_BF16 : SCAN_STREAM16;
+  const float* qs = tier == TIER_BF16 ? ix->q16.as<float>() : q;
+  rc = scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
                      ix->coarse_i.as<int64_t>(), kc, k, os, oi);
   MQ_HIP(hipGetLastError());
   if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
+  int64_t* fail = ix->tier_fail[tier].as<int64_t>();
   MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q, ix->dim,
-                     ix->coarse_s.as<float>(), kc, os, k, nq, ix->flag.as<int>());
+  const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
+  hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
+                     ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode,
+                     bf ? ix->stats16.as<unsigned>() : nullptr, ix->flag.as<int>(), fail);
   MQ_HIP(hipGetLastError());
-  int bad = 0;
-  MQ_HIP(hipMemcpyAsync(&bad, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  int n_fail = 0;
+  MQ_HIP(hipMemcpyAsync(&n_fail, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
-  if (!bad) return MQ_OK;
-  ++ix->screen_fallbacks;
-  return scan_topk(ix, SCAN_F32, q, nq, k, os, oi, s);
+  if (n_fail == 0) return MQ_OK;
+  // re-run the uncertified queries one tier down, into this tier's scratch
+  rc = ix->tier_q[tier].ensure((size_t)n_fail * ix->dim * sizeof(float));
+  if (!rc) rc = ix->tier_s[tier].ensure((size_t)n_fail * k * sizeof(float));
+  if (!rc) rc = ix->tier_i[tier].ensure((size_t)n_fail * k * sizeof(int64_t));
+  if (rc) return rc;
+  float* sq = ix->tier_q[tier].as<float>();
+  float* ss = ix->tier_s[tier].as<float>();
+  int64_t* si = ix->tier_i[tier].as<int64_t>();
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n_fail + 3) / 4)), dim3(256), 0, s, q,
+                     fail, (int64_t)n_fail, ix->dim, sq);
+  MQ_HIP(hipGetLastError());
+  if (tier == TIER_BF16 && x6_tier_ok(ix, n_fail, k)) {
+    ix->screen_passdowns += n_fail;
+    rc = search_screened(ix, TIER_X6, sq, n_fail, k, ss, si, s);
+  } else {
+    ix->screen_fallbacks += n_fail;
+    rc = search_direct(ix, sq, n_fail, k, ss, si, s);
+  }
+  if (rc) return rc;
+  const int64_t total = (int64_t)n_fail * k;
+  hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     ss, si, fail, (int64_t)n_fail, k, os, oi);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
 }
 
-// Search with queries and outputs already in device memory (asynchronous for k <= 16).
+// Search with queries and outputs already in device memory (asynchronous for k <= 16,
+// except the screened mode).
 int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                   hipStream_t s) {
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
-  // few queries: exact fp32 streaming scan, whatever the precision setting
-  if (nq <= ix->stream_max_q && ix->dim % 64 == 0 && ix->dim <= 64 * kStreamMaxNV)
+  const bool screen = ix->precision == MQ_DTYPE_F32_SCREEN;
+  if (nq <= ix->stream_max_q && stream_ok(ix)) {  // few queries: streaming scans
+    if (screen && ix->dim % 128 == 0) return search_screened(ix, TIER_BF16_STREAM, q, nq, k, os, oi, s);
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
+  }
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
-  if (ix->precision == MQ_DTYPE_F32_SCREEN && nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024)
-    return search_screened(ix, q, nq, k, os, oi, s);
+  if (screen && ix->dim % 64 == 0 && ix->dim <= 1024)
+    return search_screened(ix, TIER_BF16, q, nq, k, os, oi, s);
   return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
 }
 
@@ -953,6 +1154,13 @@ int mq_index_destroy(mq_index* ix) {
     ix->coarse_s.release();
     ix->coarse_i.release();
     ix->flag.release();
+    ix->stats16.release();
+    for (int t = 0; t < 3; ++t) {
+      ix->tier_fail[t].release();
+      ix->tier_q[t].release();
+      ix->tier_s[t].release();
+      ix->tier_i[t].release();
+    }
   }
   delete ix;
   return MQ_OK;
@@ -1130,10 +1338,11 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries) {
   return MQ_OK;
 }
 
-int mq_index_screen_fallbacks(const mq_index* ix, int64_t* n) {
+int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split) {
   clear_error();
-  MQ_CHECK_ARG(ix && n, "NULL argument");
-  *n = ix->screen_fallbacks;
+  MQ_CHECK_ARG(ix, "NULL argument");
+  if (to_direct) *to_direct = ix->screen_fallbacks;
+  if (to_split) *to_split = ix->screen_passdowns;
   return MQ_OK;
 }
 

@@ -85,7 +85,8 @@ class FlatIndex:
     def set_precision(self, dtype):
         """_lib.MQ_DTYPE_F32 (exact f32 MFMA), _lib.MQ_DTYPE_F32X6 (split-f32),
         _lib.MQ_DTYPE_BF16 (bf16 coarse scan + exact fp32 re-rank) or
-        _lib.MQ_DTYPE_F32_SCREEN (exact fp32 top-k: certified split-f32 screen + re-rank)."""
+        _lib.MQ_DTYPE_F32_SCREEN (exact fp32 top-k: certified bf16 / split-f32 screens +
+        fp32 re-rank)."""
         _lib.call("mq_index_set_precision", self._h, dtype)
 
     def set_stream_threshold(self, max_queries):
@@ -108,9 +109,16 @@ class FlatIndex:
 
     @property
     def screen_fallbacks(self):
-        """Screened searches (MQ_DTYPE_F32_SCREEN) re-run on the direct exact scan."""
+        """Screened queries (MQ_DTYPE_F32_SCREEN) re-run on the direct exact scan."""
         n = ctypes.c_int64()
-        _lib.call("mq_index_screen_fallbacks", self._h, ctypes.byref(n))
+        _lib.call("mq_index_screen_fallbacks", self._h, ctypes.byref(n), None)
+        return n.value
+
+    @property
+    def screen_passdowns(self):
+        """bf16-screened queries whose certificate failed, re-run on the split-f32 screen."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_screen_fallbacks", self._h, None, ctypes.byref(n))
         return n.value
 
     def set_timing(self, enabled=True):

@@ -294,18 +294,22 @@ def test_select_gathers_and_compacts(require_gpu):
         sub.select([6])
 
 
+@pytest.mark.parametrize("nq", [1, 3, 40, 256])
 @pytest.mark.parametrize("k", [1, 5, 50])
-def test_screened_exact_matches_direct_exact(require_gpu, golden, k):
-    """MQ_DTYPE_F32_SCREEN returns the exact fp32 top-k (split-f32 screen + fp32 re-rank,
-    certified): same ids as the direct exact scan outside tie groups, oracle parity."""
+def test_screened_exact_matches_direct_exact(require_gpu, golden, k, nq):
+    """MQ_DTYPE_F32_SCREEN returns the exact fp32 top-k through certified screens (bf16
+    shadow stream for nq <= 4, bf16 MFMA scan for batches, split-f32 for the queries
+    passed down, direct scan last): same ids as the direct exact scan outside tie groups,
+    oracle parity, scores within two fp32 dot orders."""
     f = np.load(os.path.join(golden, "flat_golden.npz"))
     c = synth.corpus(int(f["n"]), int(f["dim"]), clustered=True)
-    q, planted = synth.queries(256, c)
+    q, planted = synth.queries(nq, c)
     ref = exact_scores(q, c)
     ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
     s, i = ix.search(q, k)
     assert check_topk(i, s, ref, k) == []
-    assert ix.screen_fallbacks == 0
+    pl = planted >= 0
+    assert (i[pl, 0] == planted[pl]).all()
     ix.set_precision(_lib.MQ_DTYPE_F32)
     s2, i2 = ix.search(q, k)
     assert check_topk(i2, s2, ref, k) == []
@@ -313,13 +317,51 @@ def test_screened_exact_matches_direct_exact(require_gpu, golden, k):
 
 
 def test_screened_falls_back_when_uncertified(require_gpu):
-    """Twenty copies of the best row: the last candidate ties the k-th result, the
-    certificate cannot hold, and the batch is re-run on the direct exact scan."""
+    """Twenty copies of the best row: the last candidate ties the k-th result, no
+    certificate can hold, and the query is re-run on the direct exact scan (the bf16
+    screen passes it to the direct scan, a lone failure; the others stay certified)."""
     c = synth.corpus(4000, 768, clustered=True)
     q, _ = synth.queries(128, c)
-    c[1000:1020] = q[0]  # exact duplicates of query 0's direction
+    c[1000:1070] = q[0]  # exact duplicates of query 0's direction (more than 64)
     ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
     s, i = ix.search(q, 5)
-    assert ix.screen_fallbacks == 1
+    assert ix.screen_fallbacks >= 1
     assert i[0].tolist() == [1000, 1001, 1002, 1003, 1004]
     assert check_topk(i, s, exact_scores(q, c), 5) == []
+    before = ix.screen_fallbacks
+    s1, i1 = ix.search(q[:1], 5)  # single query: bf16 stream screen -> exact stream
+    assert ix.screen_fallbacks == before + 1
+    assert i1[0].tolist() == [1000, 1001, 1002, 1003, 1004]
+
+
+def _near_tie_rows(q, spacing, count, rng):
+    """Rows at cosine 1 - m * spacing (m = 0..count-1) from unit query q."""
+    out = []
+    for m in range(count):
+        u = rng.standard_normal(q.shape[0]).astype(np.float64)
+        u -= (u @ q) * q
+        u /= np.linalg.norm(u)
+        cm = 1.0 - m * spacing
+        out.append(cm * q + np.sqrt(1.0 - cm * cm) * u)
+    return np.array(out, np.float32)
+
+
+def test_screened_passes_near_ties_to_split_f32(require_gpu):
+    """Top-70 scores 4e-5 apart: the 5th and 64th best are 2.4e-3 apart, inside the bf16
+    screen's ~3.5e-3 bound (uncertified); the 5th and 8th 1.2e-4 apart, outside the
+    split-f32 screen's 8e-5 (certified): the 100 queries go down one tier, none reaches
+    the direct scan, and the results stay exact."""
+    rng = np.random.default_rng(5)
+    c = rng.standard_normal((30000, 768)).astype(np.float32)
+    q = rng.standard_normal((128, 768))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    for j in range(100):
+        c[j * 70:(j + 1) * 70] = _near_tie_rows(q[j], 4e-5, 70, rng)
+    q = q.astype(np.float32)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    assert ix.screen_passdowns >= 100
+    assert ix.screen_fallbacks == 0
+    assert check_topk(i, s, exact_scores(q, c), 5) == []
+    for j in range(100):
+        assert i[j].tolist() == list(range(j * 70, j * 70 + 5))
