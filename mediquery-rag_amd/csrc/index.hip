@@ -97,8 +97,14 @@ struct TopList {
 
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
-using SearchWideX6 = F32Tile<2, 2, 2, 2, true>;  // same, split-f32 arithmetic
-using SearchWideBF = F32Tile<2, 2, 2, 2, false, 2, true>;    // bf16 coarse scan
+#ifndef MQ_X6_PF
+#define MQ_X6_PF 2
+#endif
+using SearchWideX6 = F32Tile<2, 2, 2, 2, true, MQ_X6_PF>;  // same, split-f32 arithmetic
+#ifndef MQ_BF_PF
+#define MQ_BF_PF 2
+#endif
+using SearchWideBF = F32Tile<2, 2, 2, 2, false, MQ_BF_PF, true>;  // bf16 coarse scan
 using SearchNarrowBF = F32Tile<1, 4, 1, 1, false, 2, true>;  // bf16 coarse, small batches
 using SearchNarrow = F32Tile<1, 4, 1, 1>;  // 32 queries x 128 rows per block (small batches)
 
@@ -524,18 +530,17 @@ __global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restr
 //  bit 1 (KC < k_out, 16-entry thread lists for large k): same test on each thread's
 //        register list -> re-run only this merge with KC = 64.
 template <int KC, typename IdIn>
-__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs,
-                                                    const IdIn* __restrict__ ci, int n_lists,
-                                                    int64_t nq, int k_in, int k_out,
-                                                    float* __restrict__ out_s,
-                                                    int64_t* __restrict__ out_i, int list_kc,
-                                                    int* __restrict__ overflow) {
+__device__ __forceinline__ void merge_threadlists(const float* __restrict__ cs,
+                                                  const IdIn* __restrict__ ci, int n_lists,
+                                                  int64_t nq, int k_in, int k_out,
+                                                  float* __restrict__ out_s,
+                                                  int64_t* __restrict__ out_i, int list_kc,
+                                                  int* __restrict__ overflow, int64_t q) {
   constexpr int U = 8;
   __shared__ float ws[4 * MQ_MAX_K];
   __shared__ long long wi[4 * MQ_MAX_K];
   __shared__ float kth_s;
   __shared__ long long kth_i;
-  const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // local lists hold int ids; shard-merge ids are int64 -> use a 64-bit twin list
   float ls[KC];
@@ -576,11 +581,24 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
       if (hi[u] < 0 || !better(hs[u], hi[u], ls[KC - 1], li[KC - 1])) continue;
       push(hs[u], hi[u]);
       const int64_t off = ((int64_t)(l0 + 256 * u) * nq + q) * k_in;
-      for (int kk = 1; kk < k_in; ++kk) {  // rest of a sorted list, while it still beats
-        const float x = cs[off + kk];
-        const long long xi = (long long)ci[off + kk];
-        if (xi < 0 || !better(x, xi, ls[KC - 1], li[KC - 1])) break;
-        push(x, xi);
+      // rest of the sorted list while it still beats the tail, 8 entries per round of
+      // independent loads (one dependent load per entry was ~2/3 of the k_out = 64 merge)
+      for (int kk0 = 1; kk0 < k_in; kk0 += U) {
+        float xs[U];
+        long long xis[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          const bool in = kk0 + j < k_in;
+          xs[j] = in ? cs[off + kk0 + j] : -INFINITY;
+          xis[j] = in ? (long long)ci[off + kk0 + j] : -1;
+        }
+        bool stop = false;
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          stop = stop || xis[j] < 0 || !better(xs[j], xis[j], ls[KC - 1], li[KC - 1]);
+          if (!stop) push(xs[j], xis[j]);
+        }
+        if (stop) break;
       }
     }
   }
@@ -657,6 +675,149 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs
     // entries a full list dropped are worse than its last kept one: only a last entry
     // strictly better than the k_out-th result (or any full list, when fewer than k_out
     // results exist) can hide a member of the top-k
+    for (int lst = tid; lst < n_lists; lst += 256) {
+      const int64_t off = ((int64_t)lst * nq + q) * k_in + (list_kc - 1);
+      const long long xi = (long long)ci[off];
+      if (xi >= 0 && better(cs[off], xi, kth_s, kth_i)) atomicOr(overflow, 1);
+    }
+  }
+}
+
+template <int KC, typename IdIn>
+__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ cs,
+                                                    const IdIn* __restrict__ ci, int n_lists,
+                                                    int64_t nq, int k_in, int k_out,
+                                                    float* __restrict__ out_s,
+                                                    int64_t* __restrict__ out_i, int list_kc,
+                                                    int* __restrict__ overflow) {
+  merge_threadlists<KC, IdIn>(cs, ci, n_lists, nq, k_in, k_out, out_s, out_i, list_kc, overflow,
+                              blockIdx.x);
+}
+
+// K10 (threshold form, the default): one block per query.  T = the largest score such
+// that at least k_out list HEADS score >= T (a 32-step bitwise search on order-
+// preserving keys, heads held in registers); any entry scoring below T has k_out
+// strictly better heads, so the top-k_out are among the entries >= T.  Those survivors
+// (each sorted list walked while >= T; typically ~k_out of them) are gathered in LDS and
+// ranked exactly by (score desc, id asc).  Same results and overflow bit 0 as the
+// thread-list merge, which it falls back to (block-uniform) when n_lists > 4096 or more
+// than kSelCap entries tie at or above T.
+constexpr int kSelCap = 2048;
+constexpr int kSelHeads = 16;  // heads per thread: n_lists <= 4096
+
+__device__ __forceinline__ unsigned score_key(float x) {  // order-preserving, > 0
+  const unsigned b = __float_as_uint(x);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+template <int KC, typename IdIn>
+__global__ __launch_bounds__(256) void merge_select_kernel(const float* __restrict__ cs,
+                                                           const IdIn* __restrict__ ci, int n_lists,
+                                                           int64_t nq, int k_in, int k_out,
+                                                           float* __restrict__ out_s,
+                                                           int64_t* __restrict__ out_i, int list_kc,
+                                                           int* __restrict__ overflow) {
+  constexpr int U = 8;
+  __shared__ float ss[kSelCap];
+  __shared__ long long si[kSelCap];
+  __shared__ int part[4];
+  __shared__ int n_s;
+  __shared__ float kth_s;
+  __shared__ long long kth_i;
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (n_lists > 256 * kSelHeads) {
+    merge_threadlists<KC, IdIn>(cs, ci, n_lists, nq, k_in, k_out, out_s, out_i, list_kc, overflow, q);
+    return;
+  }
+  unsigned key[kSelHeads];
+#pragma unroll
+  for (int j = 0; j < kSelHeads; ++j) {
+    const int lst = tid + 256 * j;
+    key[j] = 0;  // absent list / padding entry
+    if (lst < n_lists) {
+      const int64_t off = ((int64_t)lst * nq + q) * k_in;
+      if ((long long)ci[off] >= 0) key[j] = score_key(cs[off]);
+    }
+  }
+  unsigned T = 0;
+  for (int b = 31; b >= 0; --b) {
+    const unsigned cand = T | (1u << b);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < kSelHeads; ++j) c += key[j] >= cand ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) part[wave] = c;
+    __syncthreads();
+    const int tot = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+    if (tot >= k_out) T = cand;
+  }
+  const unsigned adm = T > 1u ? T : 1u;  // fewer than k_out valid heads: every valid entry
+  if (tid == 0) {
+    n_s = 0;
+    kth_s = -INFINITY;
+    kth_i = -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSelHeads; ++j) {
+    if (key[j] < adm) continue;
+    const int64_t off = ((int64_t)(tid + 256 * j) * nq + q) * k_in;
+    for (int kk0 = 0; kk0 < k_in; kk0 += U) {
+      float xs[U];
+      long long xis[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool in = kk0 + u < k_in;
+        xs[u] = in ? cs[off + kk0 + u] : -INFINITY;
+        xis[u] = in ? (long long)ci[off + kk0 + u] : -1;
+      }
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        stop = stop || xis[u] < 0 || score_key(xs[u]) < adm;
+        if (!stop) {
+          const int pos = atomicAdd(&n_s, 1);
+          if (pos < kSelCap) {
+            ss[pos] = xs[u];
+            si[pos] = xis[u];
+          }
+        }
+      }
+      if (stop) break;
+    }
+  }
+  __syncthreads();
+  const int ns = n_s;
+  if (ns > kSelCap) {  // massive ties at the threshold: the thread-list merge handles them
+    merge_threadlists<KC, IdIn>(cs, ci, n_lists, nq, k_in, k_out, out_s, out_i, list_kc, overflow, q);
+    return;
+  }
+  // rank the survivors; valid ids are distinct, so the ranks are too
+  for (int c = tid; c < ns; c += 256) {
+    const float x = ss[c];
+    const long long xi = si[c];
+    int rank = 0;
+    for (int u = 0; u < ns; ++u) rank += better(ss[u], si[u], x, xi) ? 1 : 0;
+    if (rank < k_out) {
+      out_s[q * k_out + rank] = x;
+      out_i[q * k_out + rank] = xi;
+      if (rank == k_out - 1) {
+        kth_s = x;
+        kth_i = xi;
+      }
+    }
+  }
+  for (int r = ns + tid; r < k_out; r += 256) {  // padding past the valid results
+    out_s[q * k_out + r] = -INFINITY;
+    out_i[q * k_out + r] = -1;
+  }
+  if (overflow && list_kc < k_out) {
+    __syncthreads();
+    // as in merge_threadlists: a full list whose last kept entry beats the k_out-th
+    // result (or any full list, when fewer than k_out results exist) may hide a member
     for (int lst = tid; lst < n_lists; lst += 256) {
       const int64_t off = ((int64_t)lst * nq + q) * k_in + (list_kc - 1);
       const long long xi = (long long)ci[off];
@@ -744,8 +905,14 @@ void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int
 template <int KC, typename IdIn>
 void launch_merge(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
                   float* os, int64_t* oi, int list_kc, int* overflow, hipStream_t s) {
-  hipLaunchKernelGGL((merge_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
-                     n_lists, nq, k_in, k_out, os, oi, list_kc, overflow);
+  // k_out <= 16: register thread lists (25 us at B = 256); larger k_out: the threshold
+  // merge (k_out = 64: 38 us vs 96 us with 16-entry thread lists + overflow check)
+  if (k_out <= 16)
+    hipLaunchKernelGGL((merge_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
+                       n_lists, nq, k_in, k_out, os, oi, list_kc, overflow);
+  else
+    hipLaunchKernelGGL((merge_select_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
+                       n_lists, nq, k_in, k_out, os, oi, list_kc, overflow);
 }
 
 template <typename IdIn>
@@ -863,7 +1030,9 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq
 // check costs one 4-byte device->host read, i.e. k > 16 calls are synchronous.
 int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* os, int64_t* oi,
               hipStream_t s) {
-  int kc = kc_scan(k);
+  // the bf16 scan keeps 8-entry lists whatever k (measured: 16-entry lists cost it ~40%;
+  // k > 8 then runs with the merge's overflow check)
+  int kc = kind == SCAN_BF16 ? 8 : kc_scan(k);
   for (;;) {
     const int kl = std::min(kc, k);
     const bool check = kl < k;

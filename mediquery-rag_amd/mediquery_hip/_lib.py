@@ -12,7 +12,8 @@ try:  # load torch's HIP runtime first so the process has exactly one libamdhip6
 except Exception:  # pragma: no cover - torch is optional for host-only use
     torch = None
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmqhip.so")
+LIB_PATH = os.environ.get("MQ_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "libmqhip.so")
 
 MQ_OK = 0
 MQ_DTYPE_F32, MQ_DTYPE_BF16, MQ_DTYPE_F32X6, MQ_DTYPE_F32_SCREEN = 0, 1, 2, 3

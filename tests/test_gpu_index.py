@@ -92,12 +92,12 @@ def test_stream_kernel_overflow_rescan(require_gpu):
     np.testing.assert_allclose(s[0], 1.0, atol=1e-5)
 
 
-def test_merge_thread_list_overflow_remerge(require_gpu):
-    """k > 16 also merges with 16-entry thread lists (merge thread t reads scan lists
-    t, t+256, ...).  At B = 100 (wide tiles, 2 lists per 128-row tile: list = 2*tile +
-    half for the first G tiles) 15 copies in tile 3 (list 6) and 9 in tile 131 (list
-    262) put 24 top-k members in merge thread 6, while no scan list is full of copies:
-    the merge must re-run with 64-entry lists and stay exact."""
+def test_merge_concentrated_top_k(require_gpu):
+    """k > 16 merges by threshold (no per-thread lists).  At B = 100 (wide tiles, 2 lists
+    per 128-row tile: list = 2*tile + half for the first G tiles) 15 copies in tile 3
+    (list 6) and 9 in tile 131 (list 262) would have put 24 top-k members in one 16-entry
+    thread list of the thread-list merge; no scan list is full of copies: the result is
+    exact without a re-scan or re-merge."""
     nq, n = 100, 128 * 1024
     rng = np.random.default_rng(9)
     c = rng.standard_normal((n, 768), dtype=np.float32)
@@ -111,9 +111,24 @@ def test_merge_thread_list_overflow_remerge(require_gpu):
     s, i = ix.search(q, 30)
     assert (i[:, :24] == np.concatenate([blk_a, blk_b])).all()
     assert ix.rescans == r0
-    assert ix.remerges == m0 + 1
+    assert ix.remerges == m0
     ref = exact_scores(q[:2], c)
     assert check_topk(i[:2], s[:2], ref, 30) == []
+
+
+@pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32_SCREEN])
+def test_merge_massive_ties_fall_back_to_thread_lists(require_gpu, prec):
+    """4000 copies of the query row: every list head ties at the top score, more than
+    the threshold merge's 2048 survivor slots qualify, and the merge falls back to
+    register thread lists (and their 64-entry re-merge): ids 0..63 in id order."""
+    rng = np.random.default_rng(13)
+    c = rng.standard_normal((40000, 768), dtype=np.float32)
+    c[:4000] = c[0]
+    q = np.repeat(c[:1] / np.linalg.norm(c[0]), 100, axis=0)
+    ix = _index(c, prec)
+    s, i = ix.search(q, 64)
+    assert (i == np.arange(64)).all()
+    assert (s[:, 0] == s[:, 63]).all()
 
 
 def test_other_dims(require_gpu):
