@@ -100,6 +100,17 @@ def cpu_baseline(args, cfg, corpus_host_fn):
                                                 args.batch, c.shape[0], t_enc, t_search))}
 
 
+def workload_name(rows, batch, world):
+    """Which BASELINE.json config the sizes are (config 4 = its per-GPU shard at N=1)."""
+    if rows == 1_000_000 and batch == 256:
+        return "BASELINE config 3"
+    if rows == 100_000 and batch == 256:
+        return "BASELINE config 2"
+    if rows == 10_000_000 or (rows == 1_250_000 and batch == 1024):
+        return "BASELINE config 4" + (" (one GPU's 1.25M-row shard)" if world == 1 and rows < 10_000_000 else "")
+    return "custom"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -343,8 +354,9 @@ def main():
         "warmup": args.warmup, "ms_per_step": main_r["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (seeded corpus on device, seeded token ids, seeded BERT-base weights)",
-        "config": {"workload": "BASELINE config 3: %d x 768 fp32 corpus, batch %d/GPU (L=%d) "
-                               "embed + exact top-%d" % (args.corpus_rows, B, L, K),
+        "config": {"workload": "%s: %d x 768 fp32 corpus, batch %d/GPU (L=%d) "
+                               "embed + exact top-%d" % (workload_name(args.corpus_rows, B, world),
+                                                          args.corpus_rows, B, L, K),
                    "corpus_rows": args.corpus_rows, "rows_per_gpu": cnt, "batch_per_gpu": B,
                    "global_batch": nq_all, "seq_len": L, "k": K,
                    "encoder": "BERT-base %dL (dmeta-embedding-zh shape)" % cfg.layers,
