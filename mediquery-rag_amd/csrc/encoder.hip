@@ -167,17 +167,27 @@ __global__ __launch_bounds__(256, 2) void gemm_splitk_kernel(const float* __rest
                 coords, epi);
 }
 
-// sum_{s<S} p[s * plane] (float4), left to right; the loads go out 8 at a time so a
-// deep split does not serialise on load latency (same additions, same order).
+// sum_{s<S} p[s * plane] (float4), left to right; the loads go out 8, then 4 at a time
+// so a deep split does not serialise on load latency (same additions, same order: the
+// sum starts from -0.0f, the exact additive identity; S = 12 and 16, the split factors
+// of K = 768 and 3072, take no single-load round trip).
 __device__ __forceinline__ floatx4 sum_slabs(const float* __restrict__ p, int64_t plane, int S) {
-  floatx4 v = *reinterpret_cast<const floatx4*>(p);
-  int s = 1;
+  floatx4 v = {-0.f, -0.f, -0.f, -0.f};
+  int s = 0;
   for (; s + 8 <= S; s += 8) {
     floatx4 t[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const floatx4*>(p + (s + u) * plane);
 #pragma unroll
     for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  if (s + 4 <= S) {
+    floatx4 t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const floatx4*>(p + (s + u) * plane);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v += t[u];
+    s += 4;
   }
   for (; s < S; ++s) v += *reinterpret_cast<const floatx4*>(p + s * plane);
   return v;
@@ -253,14 +263,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(
   for (int i = 0; i < VPL; ++i) {
     const int c = t + 256 * i;
     const float* p = slab + (int64_t)row * H + c;
-    float v = p[0];
-    int sl = 1;
+    float v = -0.f;  // as sum_slabs: 8 then 4 loads in flight, same order
+    int sl = 0;
     for (; sl + 8 <= S; sl += 8) {
       float u[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) u[j] = p[(sl + j) * plane];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v += u[j];
+    }
+    if (sl + 4 <= S) {
+      float u[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u[j] = p[(sl + j) * plane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v += u[j];
+      sl += 4;
     }
     for (; sl < S; ++sl) v += p[sl * plane];
     x[i] = v + bias[c] + resid[(int64_t)row * ldr + c];
