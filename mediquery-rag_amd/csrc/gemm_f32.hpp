@@ -86,6 +86,20 @@ __device__ __forceinline__ void split3(floatx4 x, uint2 (&pl)[3]) {
   }
 }
 
+// compile-time loop: f(IC<0>{}) .. f(IC<N-1>{})
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 // One K-slice of both operands, held in registers between the global load and the
 // LDS write (T14 "issue early / write late").  Rows past M / N are clamped onto the
 // last valid row instead of being zeroed: an MFMA output element depends only on its
@@ -189,15 +203,29 @@ __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T:
   }
   const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * 16;
   const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * 16;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    floatx4 a[T::TM], b[T::TN];
+  // Two fragment sets: the ds_reads of step q+1 go out under the MFMAs of step q.  Left
+  // to itself the scheduler reads two steps at once into ONE register set, so the reads
+  // of steps 2-3 wait (WAR) for the last MFMA of step 1 and the pipe idles for an LDS
+  // round trip mid-slice.  MFMA order per accumulator is unchanged (bit-identical sums).
+  floatx4 a[2][T::TM], b[2][T::TN];
+  auto frag = [&](int q, floatx4(&fa)[T::TM], floatx4(&fb)[T::TN]) {
 #pragma unroll
     for (int tm = 0; tm < T::TM; ++tm)
-      a[tm] = *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4);
+      fa[tm] = *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4);
 #pragma unroll
     for (int tn = 0; tn < T::TN; ++tn)
-      b[tn] = *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4);
+      fb[tn] = *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4);
+  };
+  // Each step is its own scheduling block (the scheduler would otherwise pick reads of
+  // any step to interleave, or sink the reads to the end of the MFMA run): reads of q+1,
+  // then the MFMAs of q, each pinned by a sched_barrier.
+  frag(0, a[0], b[0]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = q & 1;
+    if (q + 1 < 4) frag(q + 1, a[c ^ 1], b[c ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -205,7 +233,8 @@ __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T:
 #pragma unroll
         for (int tn = 0; tn < T::TN; ++tn)
           acc[tm][tn] =
-              __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm][s], b[tn][s], acc[tm][tn], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][tm][s], b[c][tn][s], acc[tm][tn], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -252,19 +281,6 @@ struct TileOperands {
 // epi(i, acc, released_stage) runs after the last slice of tile i, with
 // `released_stage` an LDS buffer no wave reads before the next barrier (an epilogue
 // that uses it must end with a barrier).
-template <int V>
-struct IC {
-  static constexpr int value = V;
-};
-
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(IC<I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
 template <class T, int D = T::PF, class Coords, class Epi>
 __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOperands& op,
                                            Coords coords, Epi epi) {
