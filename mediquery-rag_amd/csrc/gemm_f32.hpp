@@ -155,20 +155,31 @@ __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T:
     // lane half h: k = 32h .. 32h+31 of the 64-wide slice; step q takes k = 32h + 8q + j
     const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * 16;
     const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      bf16x8 a[T::TM], b[T::TN];
+    // two fragment sets, reads of step q+1 pinned ahead of the MFMAs of step q (as in the
+    // f32 path below; a bf16 step is only TM*TN short MFMAs, so an exposed LDS round trip
+    // per step costs proportionally more here)
+    bf16x8 a[2][T::TM], b[2][T::TN];
+    auto frag = [&](int q, bf16x8(&fa)[T::TM], bf16x8(&fb)[T::TN]) {
 #pragma unroll
       for (int tm = 0; tm < T::TM; ++tm)
-        a[tm] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4));
+        fa[tm] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(as + tm * 32 * T::ROW_FLOATS + q * 4));
 #pragma unroll
       for (int tn = 0; tn < T::TN; ++tn)
-        b[tn] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4));
+        fb[tn] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const floatx4*>(bs + tn * 32 * T::ROW_FLOATS + q * 4));
+    };
+    frag(0, a[0], b[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = q & 1;
+      if (q + 1 < 4) frag(q + 1, a[c ^ 1], b[c ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < T::TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c][tm], b[c][tn], acc[tm][tn], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     return;
   }
