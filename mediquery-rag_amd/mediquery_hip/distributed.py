@@ -69,11 +69,28 @@ class ShardedSearcher:
         return torch.from_numpy(os_), torch.from_numpy(oi)
 
     def search_local_batch(self, q_local, k):
-        """DP-encoded queries: gather every rank's batch, search all, keep own rows."""
-        world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
-        allq = self.gather_queries(q_local)
-        B = q_local.shape[0]
-        return self.search(allq, k, keep=(rank * B, (rank + 1) * B))  # merge own rows only
+        """DP-encoded queries: gather every rank's batch, search all, keep own rows.
+        Ranks may hold different batch sizes (a ragged last batch): the sizes are
+        all-gathered first, every batch is padded to the largest for the one query
+        all-gather, and the padding is dropped before the scan."""
+        rank = dist.get_rank(self.group)
+        B = int(q_local.shape[0])
+        sizes = self._all_gather(torch.tensor([B], dtype=torch.int64, device=q_local.device))
+        sizes = [int(x) for x in sizes.reshape(-1).tolist()]
+        Bmax = max(sizes)
+        if Bmax != B:
+            pad = torch.zeros((Bmax - B, q_local.shape[1]), dtype=q_local.dtype, device=q_local.device)
+            q_local = torch.cat([q_local, pad])
+        g = self._all_gather(q_local)  # [world, Bmax, dim]
+        if any(b != Bmax for b in sizes):
+            allq = torch.cat([g[r, :b] for r, b in enumerate(sizes)])
+        else:
+            allq = g.reshape(-1, q_local.shape[-1])
+        start = sum(sizes[:rank])
+        if allq.shape[0] == 0:
+            e = torch.empty((0, k), device=q_local.device)
+            return e, e.to(torch.int64)
+        return self.search(allq, k, keep=(start, start + B))  # merge own rows only
 
 
 def ingest_sharded(texts, embed_fn, index_add, world=None, rank=None, group=None, chunk=4096):

@@ -10,7 +10,17 @@ Reference call sites (unchanged by the swap):
 Same contract as LangChain's Embeddings: lists of python floats, one unit-norm
 768-vector per text.  The forward runs in libmqhip.so (HIP, gfx950); nothing here
 computes embeddings on the CPU.
+
+Weights and vocabulary are never downloaded.  A real model needs BOTH a local
+safetensors file and its WordPiece vocab, given as arguments or through the
+environment (so the reference's constructor line stays unchanged):
+    MQ_WEIGHTS_PATH=/models/dmeta.safetensors MQ_VOCAB_FILE=/models/vocab.txt
+Seeded random weights with the char tokenizer (tests, benchmarks) must be asked for
+explicitly with `synthetic=True`: a silently random encoder would hand the Retrieve
+node semantically random documents.
 """
+import os
+
 import numpy as np
 
 from .compat import EmbeddingsBase
@@ -19,25 +29,50 @@ from .native import Encoder
 from .tokenizer import NativeTokenizer
 from .weights import load_safetensors
 
+ENV_WEIGHTS = "MQ_WEIGHTS_PATH"
+ENV_VOCAB = "MQ_VOCAB_FILE"
+
 
 class HipBertEmbeddings(EmbeddingsBase):
     """BERT-base CLS embeddings computed by the hand-written HIP encoder.
 
     model:        kept for signature parity with OllamaEmbeddings (informational).
-    weights_path: local safetensors with HF BERT names; None = seeded synthetic weights
-                  (the dmeta weights are not available offline).
-    vocab_file:   local WordPiece vocab; None = the deterministic char tokenizer.
+    weights_path: local safetensors with HF BERT names (default: $MQ_WEIGHTS_PATH).
+    vocab_file:   local WordPiece vocab.txt (default: $MQ_VOCAB_FILE); required with
+                  real weights - the char tokenizer would feed them meaningless ids.
+    synthetic:    True = seeded random weights + the deterministic char tokenizer
+                  (`seed`); the only way to get them.
     """
 
     def __init__(self, model="shaw/dmeta-embedding-zh", *, weights_path=None, vocab_file=None,
-                 config: BertConfig = DMETA_BASE, seed=0, device=0, batch_size=256,
-                 max_length=512, **kwargs):
+                 synthetic=False, config: BertConfig = DMETA_BASE, seed=0, device=0,
+                 batch_size=256, max_length=512, **kwargs):
         self.model = model
         self.config = config
         self.device = device
         self.batch_size = int(batch_size)
         self.max_length = min(int(max_length), config.max_positions)
-        weights = load_safetensors(weights_path, config) if weights_path else None
+        self.synthetic = bool(synthetic)
+        if self.synthetic:
+            if weights_path or vocab_file:
+                raise ValueError("synthetic=True takes no weights_path / vocab_file")
+            weights = None
+        else:
+            weights_path = weights_path or os.environ.get(ENV_WEIGHTS)
+            vocab_file = vocab_file or os.environ.get(ENV_VOCAB)
+            if not weights_path or not vocab_file:
+                raise ValueError(
+                    "HipBertEmbeddings(model=%r) needs the model's local weights AND vocab "
+                    "(weights_path=/vocab_file= or $%s/$%s; nothing is downloaded). Missing: %s. "
+                    "Pass synthetic=True for seeded random weights (tests/benchmarks only)."
+                    % (model, ENV_WEIGHTS, ENV_VOCAB,
+                       ", ".join(n for n, v in (("weights", weights_path), ("vocab", vocab_file))
+                                 if not v)))
+            for what, p in (("weights", weights_path), ("vocab", vocab_file)):
+                if not os.path.isfile(p):
+                    raise FileNotFoundError("%s file %r does not exist" % (what, p))
+            weights = load_safetensors(weights_path, config)
+        self.weights_path, self.vocab_file = weights_path, vocab_file
         self.encoder = Encoder(config, weights=weights, seed=seed, device=device)
         if vocab_file:  # C++ tokenizers of libmqhip.so
             self.tokenizer = NativeTokenizer.wordpiece(vocab_file, max_length=self.max_length)

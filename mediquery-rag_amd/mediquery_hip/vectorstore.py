@@ -13,7 +13,16 @@ on the host, keyed by row id = insertion order.  Semantics follow Chroma's defau
 "l2" space: `similarity_search_with_score` returns squared L2 distance, which for the
 unit-norm embeddings is 2 - 2*cos; `similarity_search` returns documents by ascending
 distance, ties broken by insertion order.  k > N returns N documents; an empty store
-returns [].  Errors raise (the reference's retrieve_node does not catch either).
+returns [].  The device top-k holds at most MQ_MAX_K (64) results: a search whose result
+count min(k, candidates) exceeds it raises instead of truncating.  Errors raise (the
+reference's retrieve_node does not catch either).
+
+Persistence: `mq_<collection>.json` (ids, documents, metadatas, and the name of the slab
+file) is the commit point; each write puts the rows in a fresh `mq_<collection>.<gen>.flat`
+and then atomically replaces the JSON, so a crash leaves either the old or the new store,
+never a slab/sidecar mismatch.  A directory that holds a stock Chroma database
+(`chroma.sqlite3`, written by the reference's ingest) but no sidecar is refused: it must be
+re-ingested with this store (`python src/ingest_medical.py` after the import swap).
 """
 import json
 import math
@@ -57,23 +66,44 @@ def _match(meta, where):
     return True
 
 
+def _check_k(k, n_candidates):
+    """Result count of a top-k over n_candidates rows; raises past the device limit."""
+    kk = min(int(k), int(n_candidates))
+    if kk > _lib.MQ_MAX_K:
+        raise ValueError("a search returning %d results (k=%d over %d rows) exceeds the device "
+                         "top-k limit MQ_MAX_K=%d" % (kk, k, n_candidates, _lib.MQ_MAX_K))
+    return kk
+
+
 class HipChroma(VectorStoreBase):
     _FILES = ("mq_%s.flat", "mq_%s.json")
+    FOREIGN_DB = "chroma.sqlite3"  # what langchain_chroma / chromadb persist
 
     def __init__(self, collection_name="langchain", embedding_function=None,
                  persist_directory=None, client_settings=None, collection_metadata=None,
-                 client=None, relevance_score_fn=None, *, device=0, dim=None, **kwargs):
+                 client=None, relevance_score_fn=None, *, device=0, dim=None,
+                 auto_persist=True, _ingest=False, **kwargs):
+        """auto_persist=False: writes stay in memory until `persist()` (bulk ingest)."""
         self._collection_name = collection_name
         self._embedding_function = embedding_function
         self._persist_directory = persist_directory
         self._collection_metadata = dict(collection_metadata or {})
         self.override_relevance_score_fn = relevance_score_fn
         self._device = device
+        self._auto_persist = bool(auto_persist)
         self._ids, self._texts, self._metas = [], [], []
         self._index = None
         self._dim = dim
+        self._slab_name = None
         if persist_directory and os.path.exists(self._path(1)):
             self._load()
+        elif (persist_directory and not _ingest
+              and os.path.exists(os.path.join(persist_directory, self.FOREIGN_DB))):
+            raise RuntimeError(
+                "%r holds a ChromaDB database (%s) but no %s sidecar: the MI355X store cannot "
+                "read Chroma's files. Re-run the ingest (src/ingest_medical.py) with the "
+                "mediquery_hip import swap to build it." % (persist_directory, self.FOREIGN_DB,
+                                                            self._FILES[1] % collection_name))
 
     # ---- helpers ---------------------------------------------------------------------
     @property
@@ -93,20 +123,37 @@ class HipChroma(VectorStoreBase):
             raise ValueError("embedding dim %d != collection dim %d" % (dim, self._dim))
 
     def _persist(self):
-        if not self._persist_directory:
+        if self._auto_persist:
+            self.persist()
+
+    def persist(self):
+        """Write the store under persist_directory (crash-safe, see the module doc)."""
+        if not self._persist_directory or self._index is None:
             return
-        os.makedirs(self._persist_directory, exist_ok=True)
-        self._index.save(self._path(0))
-        with open(self._path(1), "w", encoding="utf-8") as f:
-            json.dump({"dim": self._dim, "ids": self._ids, "documents": self._texts,
-                       "metadatas": self._metas, "collection_metadata": self._collection_metadata},
-                      f, ensure_ascii=False)
+        d = self._persist_directory
+        os.makedirs(d, exist_ok=True)
+        slab = "mq_%s.%s.flat" % (self._collection_name, uuid.uuid4().hex[:12])
+        self._index.save(os.path.join(d, slab))
+        side = self._path(1)
+        tmp = side + ".tmp"
+        with open(tmp, "w", encoding="utf-8") as f:
+            json.dump({"dim": self._dim, "slab": slab, "n_rows": len(self._ids), "ids": self._ids,
+                       "documents": self._texts, "metadatas": self._metas,
+                       "collection_metadata": self._collection_metadata}, f, ensure_ascii=False)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, side)  # the commit point
+        old, self._slab_name = self._slab_name, slab
+        for stale in (old, self._FILES[0] % self._collection_name):
+            if stale and stale != slab and os.path.exists(os.path.join(d, stale)):
+                os.remove(os.path.join(d, stale))
 
     def _load(self):
         with open(self._path(1), "r", encoding="utf-8") as f:
             side = json.load(f)
         self._ensure_index(side["dim"])
-        self._index.load(self._path(0))
+        self._slab_name = side.get("slab", self._FILES[0] % self._collection_name)
+        self._index.load(os.path.join(self._persist_directory, self._slab_name))
         self._ids, self._texts, self._metas = side["ids"], side["documents"], side["metadatas"]
         self._collection_metadata = side.get("collection_metadata", {})
         if len(self._index) != len(self._ids):
@@ -189,9 +236,7 @@ class HipChroma(VectorStoreBase):
             return []
         q = np.ascontiguousarray(vec, dtype=np.float32).reshape(1, -1)
         if not filter:
-            if k > _lib.MQ_MAX_K and k < n:
-                raise ValueError("k=%d exceeds the device top-k limit %d" % (k, _lib.MQ_MAX_K))
-            kk = min(k, n, _lib.MQ_MAX_K)
+            kk = _check_k(k, n)
             s, i = self._index.search(q, kk)
             return [(int(r), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
         allowed = np.array([r for r in range(n) if _match(self._metas[r], filter)], dtype=np.int64)
@@ -200,7 +245,7 @@ class HipChroma(VectorStoreBase):
         # exact filtered search: score only the allowed rows, gathered on the device into
         # a scratch index (rows bit-identical to the store's)
         sub = self._index.select(allowed)
-        kk = min(k, len(allowed), _lib.MQ_MAX_K)
+        kk = _check_k(k, len(allowed))
         s, i = sub.search(q, kk)
         sub.close()
         return [(int(allowed[r]), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
@@ -224,13 +269,13 @@ class HipChroma(VectorStoreBase):
     def similarity_search_batch(self, queries, k=DEFAULT_K):
         """Many queries in one encoder batch + one device search (the throughput path)."""
         n = 0 if self._index is None else len(self._index)
-        if n == 0 or not queries:
+        if n == 0 or not queries or k <= 0:
             return [[] for _ in queries]
+        kk = _check_k(k, n)
         if hasattr(self._embedding_function, "embed_array"):
             q = self._embedding_function.embed_array(list(queries))
         else:
             q = np.asarray(self._embedding_function.embed_documents(list(queries)), np.float32)
-        kk = min(k, n, _lib.MQ_MAX_K)
         _, ids = self._index.search(q, kk)
         return [[self._doc(int(r)) for r in row if r >= 0] for row in ids]
 
@@ -248,7 +293,7 @@ class HipChroma(VectorStoreBase):
     def from_texts(cls, texts, embedding=None, metadatas=None, ids=None,
                    collection_name="langchain", persist_directory=None, **kwargs):
         store = cls(collection_name=collection_name, embedding_function=embedding,
-                    persist_directory=persist_directory, **kwargs)
+                    persist_directory=persist_directory, _ingest=True, **kwargs)
         store.add_texts(texts, metadatas=metadatas, ids=ids)
         return store
 

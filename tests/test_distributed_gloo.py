@@ -50,7 +50,10 @@ def _worker(rank, world, port, out_q, N, K):
         # DP query path: each rank contributes half the batch
         half = NQ // world
         s2, i2 = ss.search_local_batch(torch.from_numpy(q[rank * half:(rank + 1) * half]), K)
-        out_q.put((rank, i.numpy(), s.numpy(), i2.numpy()))
+        # ragged DP batches (a short last batch): ranks hold different query counts
+        qo, qc = shard_bounds(NQ - 1, world, world - 1 - rank)
+        _, i3 = ss.search_local_batch(torch.from_numpy(q[qo:qo + qc]), K)
+        out_q.put((rank, i.numpy(), s.numpy(), (i2.numpy(), i3.numpy(), qo, qc)))
     except Exception as e:  # report instead of leaving the parent waiting
         out_q.put((rank, repr(e), None, None))
         raise
@@ -78,10 +81,14 @@ def test_sharded_search_equals_single_index(world, N, K):
     res.sort(key=lambda r: r[0])
     for r in res:
         assert not isinstance(r[1], str), r[1]
-    for rank, ids, scores, ids_dp in res:
+    offsets = [r[3][2] for r in res]
+    assert offsets == sorted(offsets, reverse=True)  # rank r holds block world-1-r
+    for rank, ids, scores, (ids_dp, ids_ragged, qo, qc) in res:
         assert check_topk(ids, scores, ref, K) == []
         half = NQ // world
         np.testing.assert_array_equal(ids_dp, ids[rank * half:(rank + 1) * half])
+        assert ids_ragged.shape == (qc, K)
+        np.testing.assert_array_equal(ids_ragged, ids[qo:qo + qc])
     for r in res[1:]:
         np.testing.assert_array_equal(res[0][1], r[1])
 

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def embeddings(require_gpu):
-    return HipBertEmbeddings(model="shaw/dmeta-embedding-zh")
+    # seeded weights + char tokenizer: the config-1 golden was made with the same
+    return HipBertEmbeddings(model="shaw/dmeta-embedding-zh", synthetic=True)
 
 
 @pytest.fixture(scope="module")
@@ -75,3 +76,41 @@ def test_batch_search_matches_single(embeddings, docs):
     for q, b in zip(qs, batch):
         single = store.similarity_search(q, k=5)
         assert [d.page_content for d in b] == [d.page_content for d in single]
+
+
+def test_k_limit_and_crash_safe_persist(embeddings, docs, tmp_path):
+    """k past the device limit raises in every path (n = 154 > 64); every
+    write commits through one atomic sidecar replace; bulk ingest can defer writes;
+    ingest into a directory holding a stock Chroma database rebuilds it as ours."""
+    db = str(tmp_path / "db")
+    store = HipChroma.from_documents(documents=docs, embedding=embeddings, persist_directory=db)
+    for call in (lambda: store.similarity_search("血糖", k=200),            # k >= n > 64
+                 lambda: store.similarity_search("血糖", k=65),
+                 lambda: store.similarity_search_batch(["血糖"], k=100),
+                 lambda: store.similarity_search("血糖", k=100, filter={"source": "《超越百岁》"})):
+        with pytest.raises(ValueError, match="MQ_MAX_K"):
+            call()
+    assert len(store.similarity_search("血糖", k=64)) == 64
+    slabs = [f for f in os.listdir(db) if f.endswith(".flat")]
+    assert len(slabs) == 1 and not any(f.endswith(".tmp") for f in os.listdir(db))
+    store.add_texts(["额外的文本"], metadatas=[{"title": "extra"}])
+    slabs2 = [f for f in os.listdir(db) if f.endswith(".flat")]
+    assert len(slabs2) == 1 and slabs2 != slabs          # new generation, old one removed
+    again = HipChroma(persist_directory=db, embedding_function=embeddings)
+    assert len(again) == 155
+    assert again.similarity_search("额外的文本", k=1)[0].metadata["title"] == "extra"
+
+    bulk_db = str(tmp_path / "bulk")
+    bulk = HipChroma.from_documents(documents=docs[:10], embedding=embeddings,
+                                    persist_directory=bulk_db, auto_persist=False)
+    assert not os.path.exists(os.path.join(bulk_db, "mq_langchain.json"))
+    bulk.persist()
+    assert len(HipChroma(persist_directory=bulk_db, embedding_function=embeddings)) == 10
+
+    old = tmp_path / "old_chroma"
+    old.mkdir()
+    (old / "chroma.sqlite3").write_bytes(b"SQLite format 3\x00")
+    with pytest.raises(RuntimeError, match="ChromaDB"):
+        HipChroma(persist_directory=str(old), embedding_function=embeddings)
+    HipChroma.from_documents(documents=docs[:5], embedding=embeddings, persist_directory=str(old))
+    assert len(HipChroma(persist_directory=str(old), embedding_function=embeddings)) == 5

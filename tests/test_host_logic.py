@@ -41,3 +41,49 @@ def test_wordpiece(tmp_path):
 def test_document_stand_in():
     d = Document(page_content="问题：x", metadata={"title": "x"})
     assert d.page_content == "问题：x" and d.metadata["title"] == "x"
+
+
+def test_k_limit_is_enforced_on_result_count():
+    """the device top-k limit applies to min(k, candidates) in every path."""
+    import pytest
+    from mediquery_hip import MQ_MAX_K
+    from mediquery_hip.vectorstore import _check_k
+    assert _check_k(5, 154) == 5
+    assert _check_k(50, 20) == 20                      # k > N returns N
+    assert _check_k(1000, MQ_MAX_K) == MQ_MAX_K
+    for k, n in ((MQ_MAX_K + 1, 1000), (1000, MQ_MAX_K + 1), (200, 100)):
+        with pytest.raises(ValueError, match="MQ_MAX_K"):
+            _check_k(k, n)
+
+
+def test_foreign_chroma_db_is_refused(tmp_path):
+    """a stock Chroma directory must not open as an empty store."""
+    import pytest
+    from mediquery_hip.vectorstore import HipChroma
+    (tmp_path / "chroma.sqlite3").write_bytes(b"SQLite format 3\x00")
+    with pytest.raises(RuntimeError, match="re-run the ingest|Re-run the ingest"):
+        HipChroma(persist_directory=str(tmp_path), embedding_function=None)
+    HipChroma(persist_directory=str(tmp_path / "fresh"))  # a new directory is fine
+
+
+def test_embeddings_refuse_silent_synthetic(tmp_path, monkeypatch):
+    """the real model name without local weights + vocab raises; synthetic
+    weights need synthetic=True; weights without a vocab raise."""
+    import pytest
+    from mediquery_hip.embeddings import ENV_VOCAB, ENV_WEIGHTS, HipBertEmbeddings
+    monkeypatch.delenv(ENV_WEIGHTS, raising=False)
+    monkeypatch.delenv(ENV_VOCAB, raising=False)
+    with pytest.raises(ValueError, match="synthetic=True"):
+        HipBertEmbeddings(model="shaw/dmeta-embedding-zh")
+    w = tmp_path / "w.safetensors"
+    w.write_bytes(b"")
+    with pytest.raises(ValueError, match="vocab"):
+        HipBertEmbeddings(weights_path=str(w))
+    monkeypatch.setenv(ENV_WEIGHTS, str(w))
+    with pytest.raises(ValueError, match="vocab"):
+        HipBertEmbeddings()
+    monkeypatch.setenv(ENV_VOCAB, str(tmp_path / "missing.txt"))
+    with pytest.raises(FileNotFoundError):
+        HipBertEmbeddings()
+    with pytest.raises(ValueError, match="synthetic"):
+        HipBertEmbeddings(synthetic=True, weights_path=str(w))

@@ -30,7 +30,7 @@ def main():
         base = [d["page_content"] for d in json.load(f)["docs"]]
     rng = np.random.default_rng(0)
     texts = [base[i] for i in rng.integers(0, len(base), args.docs)]
-    emb = HipBertEmbeddings()
+    emb = HipBertEmbeddings(synthetic=True)
     ix = FlatIndex(dim=768, capacity=args.docs)
     emb.embed_array(texts[:512])  # warm-up (graph capture per shape happens in the run too)
     _, mask = emb.tokenizer(texts)
