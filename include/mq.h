@@ -108,6 +108,12 @@ int mq_index_set_precision(mq_index* ix, int dtype);
 /* Batches of at most `max_queries` queries (default 4, 0..16; dim % 64 == 0, dim <= 1024)
  * use the streaming fp32 kernel instead of the MFMA tiles, whatever the precision. */
 int mq_index_set_stream_threshold(mq_index* ix, int max_queries);
+/* Batched bf16 candidate scans (MQ_DTYPE_F32_SCREEN batches, MQ_DTYPE_BF16) of more than
+ * 64 queries over >= 65536 rows with dim 256/512/768: 1 (default) = the threshold scan
+ * (sample pass -> per-query threshold -> one streaming pass keeping the rows that clear
+ * it -> top-kc of the survivors), 0 = the tiled scan with per-lane lists + merge.
+ * Same candidates either way up to bf16-score ties at the kc-th place. */
+int mq_index_set_threshold_scan(mq_index* ix, int enabled);
 /* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
  * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);

@@ -13,6 +13,8 @@
 
 #include "common.hpp"
 #include "gemm_f32.hpp"
+#include "thresh.hpp"
+#include "topk.hpp"
 
 namespace mq {
 
@@ -56,45 +58,6 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 }
 
 // ================================================ K9: fused score + top-k ======
-// Register-resident running top-KC list per lane, kept sorted by (score desc, id asc).
-template <int KC>
-struct TopList {
-  float s[KC];
-  int id[KC];
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      s[i] = -INFINITY;
-      id[i] = -1;
-    }
-  }
-  __device__ __forceinline__ bool beats_tail(float x, int xi) const {
-    return better(x, xi, s[KC - 1], id[KC - 1]);
-  }
-  // Branch-free bubble insertion with static indices (stays in VGPRs).
-  __device__ __forceinline__ void insert(float x, int xi) {
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const bool sw = better(x, xi, s[i], id[i]);
-      const float ts = s[i];
-      const int ti = id[i];
-      s[i] = sw ? x : ts;
-      id[i] = sw ? xi : ti;
-      x = sw ? ts : x;
-      xi = sw ? ti : xi;
-    }
-  }
-  __device__ __forceinline__ void pop_front() {
-#pragma unroll
-    for (int i = 0; i + 1 < KC; ++i) {
-      s[i] = s[i + 1];
-      id[i] = id[i + 1];
-    }
-    s[KC - 1] = -INFINITY;
-    id[KC - 1] = -1;
-  }
-};
-
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
 #ifndef MQ_X6_PF
@@ -885,6 +848,8 @@ struct mq_index {
   int64_t screen_fallbacks = 0;  // screened queries re-run on the direct exact scan
   int64_t screen_passdowns = 0;  // bf16-screened queries re-run on the split-f32 screen
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
+  bool thresh_scan = true;  // batched bf16 screens use the threshold scan (K9t)
+  DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t: sample maxima, tau, survivors
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -1098,7 +1063,8 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
 // bf16 shadow of the stored rows, mirrored lazily (rows added since the last bf16 search),
 // with the rounding maxima the bf16 screens certify against (reset on a rebuild).
 int ensure_shadow(mq_index* ix, hipStream_t s) {
-  int rc = ix->rows16.ensure((size_t)ix->cap * ix->dim * 2);
+  // padded to whole 32-row blocks: the threshold scan (K9t) reads blocks unclamped
+  int rc = ix->rows16.ensure((size_t)(ix->cap + kTsRows) * ix->dim * 2);
   if (!rc) rc = ix->stats16.ensure(2 * sizeof(unsigned));
   if (rc) return rc;
   if (ix->n16 < ix->n) {
@@ -1124,6 +1090,42 @@ int queries_to_bf16(mq_index* ix, const float* q, int64_t nq, hipStream_t s) {
   return MQ_OK;
 }
 
+// K9t: bf16 top-kc candidates of a batch by the threshold scan.  Sample pass (every
+// kTsPeriod-th block, per-list maxima) -> tau per query -> full pass appending the rows
+// that clear tau -> per-query select of the best kc survivors.  Stage 0 of the timeline
+// = the two scans, stage 1 = tau + select.
+bool thresh_ok(const mq_index* ix, int64_t nq) {
+  const int nch = ix->dim / 64;
+  return ix->thresh_scan && nq > 64 && ix->dim % 64 == 0 && (nch == 4 || nch == 8 || nch == 12) &&
+         ix->n >= kTsMinRows && ix->n < (1ll << 31);
+}
+
+int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
+                hipStream_t s) {
+  const size_t n_lists = 2 * (size_t)ix->num_cus;
+  int rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
+  if (!rc) rc = ix->ts_tau.ensure(nq * sizeof(float));
+  if (!rc) rc = ix->ts_count.ensure(nq * sizeof(int));
+  if (!rc) rc = ix->ts_cs.ensure((size_t)nq * kTsCap * sizeof(float));
+  if (!rc) rc = ix->ts_ci.ensure((size_t)nq * kTsCap * sizeof(int));
+  if (rc) return rc;
+  ThreshArgs a{q16, (int)nq, ix->rows16.as<unsigned char>(), ix->n, ix->dim, ix->num_cus, kc,
+               ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
+               ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi};
+  if (ix->tl.used > 4096) ix->tl.drain();
+  launch_thresh(a, s, &ix->tl);
+  ix->tl.close(s);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+// the bf16 candidate scan of a batch: K9t when it applies, else the tiled K9 + K10
+int bf16_candidates(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
+                    hipStream_t s) {
+  if (thresh_ok(ix, nq)) return thresh_topk(ix, q16, nq, kc, os, oi, s);
+  return scan_topk(ix, SCAN_BF16, q16, nq, kc, os, oi, s);
+}
+
 // Config 5: bf16 coarse scan for the best `kc` rows per query (kc = max(2k, 50) capped
 // at MQ_MAX_K and n), then an exact fp32 re-rank of those candidates to the final top-k.
 int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
@@ -1134,8 +1136,8 @@ int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* o
   const int kc = (int)std::min<int64_t>(std::max(2 * k, 50), std::min<int64_t>(MQ_MAX_K, ix->n));
   rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
   if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
-  if (!rc) rc = scan_topk(ix, SCAN_BF16, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(),
-                          ix->coarse_i.as<int64_t>(), s);
+  if (!rc) rc = bf16_candidates(ix, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(),
+                                ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
                      ix->coarse_i.as<int64_t>(), kc, k, os, oi);
@@ -1189,7 +1191,8 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   if (rc) return rc;
   const int kind = tier == TIER_X6 ? SCAN_X6 : tier == TIER_BF16 ? SCAN_BF16 : SCAN_STREAM16;
   const float* qs = tier == TIER_BF16 ? ix->q16.as<float>() : q;
-  rc = scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
+  rc = kind == SCAN_BF16 ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
+                         : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
                      ix->coarse_i.as<int64_t>(), kc, k, os, oi);
@@ -1504,6 +1507,14 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries) {
                max_queries);
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->stream_max_q = max_queries;
+  return MQ_OK;
+}
+
+int mq_index_set_threshold_scan(mq_index* ix, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->thresh_scan = enabled != 0;
   return MQ_OK;
 }
 

@@ -64,6 +64,7 @@ SIGNATURES = {
     "mq_index_data": (_I, [_P, _PP]),
     "mq_index_set_precision": (_I, [_P, _I]),
     "mq_index_set_stream_threshold": (_I, [_P, _I]),
+    "mq_index_set_threshold_scan": (_I, [_P, _I]),
     "mq_index_rescans": (_I, [_P, _P, _P]),
     "mq_index_screen_fallbacks": (_I, [_P, _P, _P]),
     "mq_index_set_timing": (_I, [_P, _I]),

@@ -93,6 +93,10 @@ class FlatIndex:
         """Batches of <= max_queries (0..16) use the streaming fp32 kernel (K9s)."""
         _lib.call("mq_index_set_stream_threshold", self._h, int(max_queries))
 
+    def set_threshold_scan(self, enabled=True):
+        """Batched bf16 candidate scans: threshold scan (K9t, default) or tiled lists."""
+        _lib.call("mq_index_set_threshold_scan", self._h, int(bool(enabled)))
+
     @property
     def rescans(self):
         """Searches whose k > 16 list-overflow check fired (re-scanned with 64 lists)."""

@@ -1,0 +1,114 @@
+"""GPU parity of K9t, the bf16 threshold scan (thresh.hip) that produces the candidates of
+batched bf16 searches over >= 65536 rows: the certified screen's first tier
+(MQ_DTYPE_F32_SCREEN) and BASELINE config 5's coarse scan (MQ_DTYPE_BF16).  Exact mode
+must return the oracle's top-k (tie-group aware) whichever candidate scan ran; the
+approximate mode must agree with the tiled candidate scan it replaces."""
+import numpy as np
+import pytest
+
+from mediquery_hip import _lib, synth
+from mediquery_hip.native import FlatIndex
+from oracle.flat import check_topk, exact_scores
+
+pytestmark = pytest.mark.gpu
+
+
+def _index(rows, prec):
+    ix = FlatIndex(dim=rows.shape[1])
+    ix.add(rows)
+    ix.set_precision(prec)
+    return ix
+
+
+@pytest.mark.parametrize("n,nq,k", [(70001, 65, 5), (70001, 256, 5), (100000, 300, 50),
+                                    (65536, 512, 16), (131075, 257, 1)])
+def test_screen_with_threshold_scan_is_exact(require_gpu, n, nq, k):
+    """Ragged last block (70001, 131075 rows), one and several 256-query groups, ragged
+    query groups (65, 257, 300): exact top-k = oracle; same ids with the tiled scan."""
+    c = synth.corpus(n, 768, seed=n, clustered=True)
+    q, planted = synth.queries(nq, c, seed=nq)
+    ref = exact_scores(q, c)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, k)
+    assert check_topk(i, s, ref, k) == []
+    pl = planted >= 0
+    assert (i[pl, 0] == planted[pl]).all()
+    ix.set_threshold_scan(False)
+    s2, i2 = ix.search(q, k)
+    assert check_topk(i2, s2, ref, k) == []
+    np.testing.assert_allclose(s, s2, atol=1e-6)
+
+
+@pytest.mark.parametrize("dim", [256, 512])
+def test_threshold_scan_other_widths(require_gpu, dim):
+    c = synth.corpus(80000, dim, seed=dim, clustered=True)
+    q, planted = synth.queries(200, c, seed=1)
+    ref = exact_scores(q, c)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    assert check_topk(i, s, ref, 5) == []
+    ix.set_precision(_lib.MQ_DTYPE_BF16)
+    s, i = ix.search(q, 10)
+    assert check_topk(i, s, ref, 10) == []
+
+
+def test_config5_coarse_candidates_match_tiled_scan(require_gpu):
+    """MQ_DTYPE_BF16, k = 50 (64 coarse candidates): the threshold scan and the tiled
+    scan pick the same bf16 top-64 up to bf16-score ties at the 64th place (the two
+    kernels sum the k-dimension in different orders), so the re-ranked top-50 agree on
+    nearly every query, and recall vs exact fp32 stays >= 0.98."""
+    n, nq, k = 120000, 256, 50
+    c = synth.corpus(n, 768, seed=7, clustered=True)
+    q, planted = synth.queries(nq, c, seed=7)
+    ix = _index(c, _lib.MQ_DTYPE_BF16)
+    s, i = ix.search(q, k)
+    ix.set_threshold_scan(False)
+    s2, i2 = ix.search(q, k)
+    same = sum(set(a.tolist()) == set(b.tolist()) for a, b in zip(i, i2))
+    assert same >= 0.99 * nq, same
+    ref = exact_scores(q, c)
+    got = np.take_along_axis(ref, i, axis=1)
+    np.testing.assert_allclose(s, got, rtol=0, atol=1e-5)
+    exact = np.argsort(-ref, axis=1, kind="stable")[:, :k]
+    hits = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(i, exact))
+    assert hits / (nq * k) >= 0.98
+    pl = planted >= 0
+    assert (i[pl, 0] == planted[pl]).all()
+
+
+def test_threshold_scan_survivor_overflow_passes_down(require_gpu):
+    """5000 copies of one direction: query 0 has more survivors than the 4096 kept, so
+    its candidate set is incomplete; the select marks the bound +inf, the certificate
+    fails and the query is re-run one tier down.  Results stay exact for every query."""
+    c = synth.corpus(90000, 768, seed=3, clustered=True)
+    q, _ = synth.queries(128, c, seed=3)
+    c[20000:25000] = q[0]  # exact duplicates: 5000 rows tie at the top for query 0
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    assert ix.screen_passdowns + ix.screen_fallbacks >= 1
+    assert i[0].tolist() == [20000, 20001, 20002, 20003, 20004]
+    assert check_topk(i, s, exact_scores(q, c), 5) == []
+
+
+def test_threshold_scan_full_size_planted(require_gpu):
+    """BASELINE config 3 size through the default screen (the bench's search): 1M x 768,
+    B = 256, k = 5 - planted queries find their rows and nothing falls back."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rows = synth.corpus_device(1_000_000, 768, dev)
+    q, planted = synth.queries_device(256, rows)
+    ix = FlatIndex(dim=768, capacity=1_000_000)
+    ix.add_device(rows)
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    s = torch.empty((256, 5), dtype=torch.float32, device=dev)
+    i = torch.empty((256, 5), dtype=torch.int64, device=dev)
+    ix.search_device(q, 5, s, i)
+    torch.cuda.synchronize()
+    pl = planted >= 0
+    assert bool((i[pl, 0] == planted[pl]).all())
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    s2, i2 = torch.empty_like(s), torch.empty_like(i)
+    ix.search_device(q, 5, s2, i2)
+    torch.cuda.synchronize()
+    assert bool((i == i2).all())
+    assert ix.screen_fallbacks == 0
