@@ -375,27 +375,29 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  // four candidates per wave per round, their row loads in flight together
-  for (int c0 = wave * 4; c0 < kc; c0 += 16) {
-    long long id[4];
-    float acc[4];
+  // eight candidates per wave per round, their row loads in flight together (the
+  // gathered rows come from HBM: the round is latency-bound, so more in flight per lane)
+  constexpr int U = 8;
+  for (int c0 = wave * U; c0 < kc; c0 += 4 * U) {
+    long long id[U];
+    float acc[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       id[u] = c0 + u < kc ? cand[q * kc + c0 + u] : -1;
       acc[u] = 0.f;
     }
     for (int i = lane; i < dim / 4; i += 64) {
       const floatx4 a = q4[i];
-      floatx4 b[4];
+      floatx4 b[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        b[u] = id[u] >= 0 ? reinterpret_cast<const floatx4*>(rows + id[u] * dim)[i] : floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < U; ++u)
+        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
         acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
       if (lane == 0 && c0 + u < kc) {

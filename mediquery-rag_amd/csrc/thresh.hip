@@ -3,6 +3,11 @@
 // config 5's coarse scan, MQ_DTYPE_BF16) - the top-k half of Chroma's similarity_search
 // (reference src/agents/nodes.py:93) at batch scale.  See DESIGN.md §4.
 #include "gemm_f32.hpp"
+
+#ifndef MQ_TS_DBG  // measurement builds only (wrong results): 1 = stream only, 2 = multiply
+                   // only, 4 = no fragment reads, 8 = no barrier
+#define MQ_TS_DBG 0
+#endif
 #include "thresh.hpp"
 #include "topk.hpp"
 
@@ -37,19 +42,28 @@ constexpr int kTsRank = 8;       // tau = 8th largest list maximum of the sample
 
 enum { TS_MAX = 0, TS_APPEND = 1 };
 
+constexpr int kTsWaveSurv = 96;  // LDS survivor slots per wave (TS_APPEND)
+struct Survivor {
+  float s;
+  int row;
+  int q;
+};
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// One LDS-DMA wave-instruction: 16 B from each lane's `src` to LDS[lds_dst + 16 lane].
+// One LDS-DMA wave-instruction: 16 B from base + voff (per lane) to LDS[lds_dst + 16 lane].
 // Issued as inline asm: hipcc tracks a compiler-visible LDS-DMA as a pending LDS write
 // and waits vmcnt(0) before every later ds_read of the same array, which would drain the
-// ring's prefetch each block.  Completion is counted by hand (s_waitcnt vmcnt(N)).
-__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
+// ring's prefetch each block.  Completion is counted by hand (s_waitcnt vmcnt(N)).  The
+// SGPR-base form keeps one 32-bit VGPR per address (the kernel runs at ~240 VGPRs: a
+// spill reload inside the loop would wait vmcnt(0) and serialise the ring).
+__device__ __forceinline__ void glds16(const void* base, unsigned voff, unsigned lds_dst) {
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+      : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
       : "memory");
 }
 
@@ -63,7 +77,11 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
                                                // whole blocks: no row clamping)
   constexpr int DMA_PER_WAVE = NCH * 4 / kTsWaves;
   static_assert(NCH % 2 == 0 && DMA_PER_WAVE * kTsWaves == NCH * 4, "8 waves share a block's DMAs");
-  __shared__ __attribute__((aligned(1024))) unsigned char ring[kTsBufs * BLK_B];
+  // one LDS array: the row ring, then each wave's survivor list (TS_APPEND)
+  constexpr int SURV_B = MODE == TS_APPEND ? kTsWaves * kTsWaveSurv * (int)sizeof(Survivor) : 0;
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[kTsBufs * BLK_B + SURV_B];
+  Survivor* surv = reinterpret_cast<Survivor*>(ring + kTsBufs * BLK_B) + (threadIdx.x >> 6) * kTsWaveSurv;
+  int n_surv = 0;  // wave-uniform
   const unsigned ring_lds = (unsigned)(uintptr_t)(lds_void_t*)ring;  // LDS byte address
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -99,15 +117,15 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
 #pragma unroll
   for (int v = 0; v < 2; ++v)
     dofs[v] = (lane >> 3) * ROW_B + (((lane & 7) ^ ((4 * v + (lane >> 4)) & 7)) * 16);
-  auto issue = [&](int i, int buf) __attribute__((always_inline)) {
+  auto issue_one = [&](int i, int buf, int tt) __attribute__((always_inline)) {
     const int64_t j = first + (int64_t)min(i, nb - 1) * stride;  // past the end: re-read the last
-    const unsigned char* base = C + j * BLK_B;
+    const int d = wave * DMA_PER_WAVE + tt;
+    glds16(C + j * BLK_B, dofs[d & 1] + (unsigned)((d & 3) * 8 * ROW_B + (d >> 2) * 128),
+           ring_lds + buf * BLK_B + d * 1024);
+  };
+  auto issue = [&](int i, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int tt = 0; tt < DMA_PER_WAVE; ++tt) {
-      const int d = wave * DMA_PER_WAVE + tt;
-      const unsigned char* g = base + ((d & 3) * 8 * ROW_B + (d >> 2) * 128) + dofs[d & 1];
-      glds16(g, ring_lds + buf * BLK_B + d * 1024);
-    }
+    for (int tt = 0; tt < DMA_PER_WAVE; ++tt) issue_one(i, buf, tt);
   };
   // A-fragment read offsets: row `col` of the block, slot (2s + h) ^ ((col >> 1) & 7)
   const int rbase = (col >> 3) * 1024 + (col & 7) * 128;
@@ -121,28 +139,38 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   const bool active = qw0 < nq;
   for (int i = 0; i < nb; ++i) {
     // own DMAs of block i landed (block i+1's may still fly), then everyone's, and every
-    // wave is done reading block i-1, whose buffer the next issue refills
+    // wave is done reading block i-1, whose buffer this iteration refills
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_WAVE) : "memory");
-    __builtin_amdgcn_s_barrier();
-    issue(i + 2, (i + 2) % kTsBufs);
-    if (!active) continue;
+    if (!(MQ_TS_DBG & 8)) __builtin_amdgcn_s_barrier();
+    if (!active || (MQ_TS_DBG & 1)) {
+      issue(i + 2, (i + 2) % kTsBufs);
+      continue;
+    }
     const unsigned char* blk = ring + (i % kTsBufs) * BLK_B + rbase;
     floatx16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    // fragment reads run two steps ahead of the MFMA chain
-    bf16x8 a[3];
+    // Hand-scheduled chain: fragment reads run three MFMA steps ahead (the compiler's own
+    // order reads one step ahead and waits out the LDS latency before every other MFMA),
+    // and block i+2's DMAs are spread over the chain, one every 8 steps, instead of
+    // delaying its start.
+    bf16x8 a[4];
     auto frag = [&](int st) __attribute__((always_inline)) {
       const int c = st >> 2, s = st & 3;
       return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uintx4*>(blk + c * 4096 + (((2 * s + h) ^ rx) * 16)));
     };
     a[0] = frag(0);
     a[1] = frag(1);
-#pragma unroll
-    for (int st = 0; st < NCH * 4; ++st) {
-      if (st + 2 < NCH * 4) a[(st + 2) % 3] = frag(st + 2);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[st % 3], qf[st], acc, 0, 0, 0);
-    }
+    a[2] = frag(2);
+    static_for<NCH * 4>([&](auto sc) {
+      constexpr int st = decltype(sc)::value;
+      if constexpr (st % 8 == 0 && st / 8 < DMA_PER_WAVE && !(MQ_TS_DBG & 2))
+        issue_one(i + 2, (i + 2) % kTsBufs, st / 8);
+      if constexpr (st + 3 < NCH * 4) a[(st + 3) & 3] = (MQ_TS_DBG & 4) ? qf[(st + 5) % (NCH * 4)] : frag(st + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[st & 3], qf[st], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
     const int64_t row0 = (first + (int64_t)i * stride) * kTsRows;
     const bool full = row0 + kTsRows <= n_rows;
     if constexpr (MODE == TS_MAX) {
@@ -152,19 +180,32 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
         if (full || row < n_rows) mx = fmaxf(mx, acc[e]);
       }
     } else {
+      // survivors go to this wave's LDS list (a ballot + lane prefix picks the slots);
+      // global slots are claimed only after the loop, so no returning atomic - whose
+      // vmcnt(0) would drain the ring - ever runs inside it
       bool any = false;
 #pragma unroll
       for (int e = 0; e < 16; ++e) any |= acc[e] >= t;
-      if (any && qvalid) {  // rare: ~128 survivors per query over the whole corpus
+      if (__builtin_amdgcn_ballot_w64(any && qvalid)) {  // rare: ~128 survivors per query
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int64_t row = row0 + acc_row(0, e, lane);
-          if (acc[e] >= t && row < n_rows) {
-            const int slot = atomicAdd(count + q, 1);
-            if (slot < kTsCap) {
-              cs[(int64_t)q * kTsCap + slot] = acc[e];
-              ci[(int64_t)q * kTsCap + slot] = (int)row;
+          const bool hit = acc[e] >= t && row < n_rows && qvalid;
+          const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+          if (m) {
+            const int pos = n_surv + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+            if (hit) {
+              if (pos < kTsWaveSurv) {
+                surv[pos] = Survivor{acc[e], (int)row, q};
+              } else {  // list full: straight to global (drains the ring; rarer still)
+                const int slot = atomicAdd(count + q, 1);
+                if (slot < kTsCap) {
+                  cs[(int64_t)q * kTsCap + slot] = acc[e];
+                  ci[(int64_t)q * kTsCap + slot] = (int)row;
+                }
+              }
             }
+            n_surv += __builtin_popcountll(m);
           }
         }
       }
@@ -172,7 +213,16 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-read DMAs
   if constexpr (MODE == TS_MAX) {
-    if (qvalid) lmax[((int64_t)blockIdx.x * 2 + h) * nq + q] = mx;
+    if (qvalid) lmax[(int64_t)q * (2 * gridDim.x) + blockIdx.x * 2 + h] = mx;  // [q][list]
+  } else {
+    for (int j = lane; j < min(n_surv, kTsWaveSurv); j += 64) {  // flush the wave's list
+      const Survivor v = surv[j];
+      const int slot = atomicAdd(count + v.q, 1);
+      if (slot < kTsCap) {
+        cs[(int64_t)v.q * kTsCap + slot] = v.s;
+        ci[(int64_t)v.q * kTsCap + slot] = v.row;
+      }
+    }
   }
 }
 
@@ -189,7 +239,7 @@ __global__ __launch_bounds__(256) void bf16_tau_kernel(const float* __restrict__
   TopList<kTsRank> t;
   t.init();
   for (int l = lane; l < n_lists; l += 64) {
-    const float x = lmax[(int64_t)l * nq + q];
+    const float x = lmax[(int64_t)q * n_lists + l];
     if (t.beats_tail(x, l)) t.insert(x, l);
   }
   float kth = -INFINITY;

@@ -18,7 +18,7 @@ struct ThreshArgs {
   int dim;                    // 256, 512 or 768
   int num_cus;
   int kc;                     // candidates per query (<= MQ_MAX_K)
-  float* lmax;                // [2 * num_cus][nq] sample-pass list maxima
+  float* lmax;                // [nq][2 * num_cus] sample-pass list maxima
   float* tau;                 // [nq]
   int* count;                 // [nq]
   float* cs;                  // [nq][kTsCap] survivor scores
