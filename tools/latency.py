@@ -46,12 +46,15 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--exact-direct", action="store_true", help="search with MQ_DTYPE_F32 (default: the screen)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     corpus = synth.corpus_device(args.rows, 768, dev)
     ix = FlatIndex(dim=768, capacity=args.rows, device=0)
     ix.add_device(corpus)
     del corpus
+    from mediquery_hip import _lib
+    ix.set_precision(_lib.MQ_DTYPE_F32 if args.exact_direct else _lib.MQ_DTYPE_F32_SCREEN)
     enc = Encoder(DMETA_BASE, device=0)
     ids_np, mask_np = synth.token_batch(1, 32)
     ids = torch.from_numpy(ids_np).to(dev)
