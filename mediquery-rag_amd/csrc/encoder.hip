@@ -757,8 +757,19 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     // rows this layer carries past attention: all M tokens, or the B CLS rows
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
-    gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
-                   ST_QKV, s);
+    if (cls_only && L > 1) {
+      // only the CLS rows need queries: K and V for every token ([M, 2H] into qkv columns
+      // H..3H), Q for the B CLS rows (every L-th row of x into row b*L of qkv)
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0,
+                         e->qkv.p + H, 3 * H, M, 2 * H, H},
+                     ST_QKV, s);
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, L * H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, L * 3 * H,
+                         B, H, H},
+                     ST_QKV, s);
+    } else {
+      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
+                     ST_QKV, s);
+    }
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,

@@ -4,7 +4,7 @@
 # mixed with trace domains (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950).
 # Summaries: python3 tools/summarize_profiles.py gpurun_out/prof_<round> profiles/<round>
 set -euo pipefail
-R=${1:-r1}
+R=${1:-r2}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
