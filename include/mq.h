@@ -190,6 +190,10 @@ int mq_encoder_embed(mq_encoder* enc, const int32_t* ids, const int32_t* mask, i
 typedef struct mq_tokenizer mq_tokenizer;
 int mq_tokenizer_create_wordpiece(const char* vocab_path, int lower_case, int max_length,
                                   mq_tokenizer** out);
+/* The same WordPiece tokenizer over an in-memory vocabulary: tokens[i] is the NUL-terminated
+ * UTF-8 token of id i (e.g. the vocab a GGUF model file embeds). */
+int mq_tokenizer_create_wordpiece_tokens(const char* const* tokens, int n_tokens, int lower_case,
+                                         int max_length, mq_tokenizer** out);
 int mq_tokenizer_create_char(int vocab_size, int max_length, mq_tokenizer** out);
 int mq_tokenizer_destroy(mq_tokenizer* tok);
 /* Encode n NUL-terminated UTF-8 texts.  ids / mask must hold n * max(max_length, pad_to)

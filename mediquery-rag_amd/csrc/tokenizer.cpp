@@ -355,6 +355,35 @@ int mq_tokenizer_create_char(int vocab_size, int max_length, mq_tokenizer** out)
   return MQ_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// WordPiece tokenizer over `tokens` in id order (a repeated token keeps its last index,
+// as HF load_vocab does).
+std::unique_ptr<mq_tokenizer> make_wordpiece(std::vector<std::string>& tokens, int lower_case,
+                                             int max_length) {
+  auto t = std::make_unique<mq_tokenizer>();
+  t->wordpiece = true;
+  t->lower = lower_case != 0;
+  t->max_length = max_length;
+  int idx = 0;
+  for (std::string& tok : tokens) t->vocab[std::move(tok)] = idx++;
+  t->vocab_size = idx;
+  auto get = [&](const char* k, int dflt) {
+    auto it = t->vocab.find(k);
+    return it == t->vocab.end() ? dflt : it->second;
+  };
+  t->unk = get("[UNK]", kUnk);
+  t->cls = get("[CLS]", kCls);
+  t->sep = get("[SEP]", kSep);
+  return t;
+}
+
+}  // namespace
+
+extern "C" {
+
 int mq_tokenizer_create_wordpiece(const char* vocab_path, int lower_case, int max_length,
                                   mq_tokenizer** out) {
   mq::clear_error();
@@ -367,25 +396,33 @@ int mq_tokenizer_create_wordpiece(const char* vocab_path, int lower_case, int ma
     mq::set_error("cannot open vocab file %s", vocab_path);
     return MQ_EIO;
   }
-  auto t = std::make_unique<mq_tokenizer>();
-  t->wordpiece = true;
-  t->lower = lower_case != 0;
-  t->max_length = max_length;
+  std::vector<std::string> tokens;
   std::string line;
-  int idx = 0;
   while (std::getline(f, line)) {
     if (!line.empty() && line.back() == '\r') line.pop_back();
-    t->vocab[line] = idx++;  // a repeated token keeps its last index, as HF load_vocab
+    tokens.push_back(line);
   }
-  t->vocab_size = idx;
-  auto get = [&](const char* k, int dflt) {
-    auto it = t->vocab.find(k);
-    return it == t->vocab.end() ? dflt : it->second;
-  };
-  t->unk = get("[UNK]", kUnk);
-  t->cls = get("[CLS]", kCls);
-  t->sep = get("[SEP]", kSep);
-  *out = t.release();
+  *out = make_wordpiece(tokens, lower_case, max_length).release();
+  return MQ_OK;
+}
+
+int mq_tokenizer_create_wordpiece_tokens(const char* const* tokens, int n_tokens, int lower_case,
+                                         int max_length, mq_tokenizer** out) {
+  mq::clear_error();
+  if (!out || !tokens || n_tokens <= 0 || max_length < 2) {
+    mq::set_error("bad wordpiece tokenizer arguments");
+    return MQ_EINVAL;
+  }
+  std::vector<std::string> v;
+  v.reserve((size_t)n_tokens);
+  for (int i = 0; i < n_tokens; ++i) {
+    if (!tokens[i]) {
+      mq::set_error("token %d is NULL", i);
+      return MQ_EINVAL;
+    }
+    v.emplace_back(tokens[i]);
+  }
+  *out = make_wordpiece(v, lower_case, max_length).release();
   return MQ_OK;
 }
 

@@ -83,6 +83,7 @@ SIGNATURES = {
     "mq_encoder_read_timing": (_I, [_P, _P, _I]),
     "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),
     "mq_tokenizer_create_wordpiece": (_I, [ctypes.c_char_p, _I, _I, _PP]),
+    "mq_tokenizer_create_wordpiece_tokens": (_I, [ctypes.POINTER(ctypes.c_char_p), _I, _I, _I, _PP]),
     "mq_tokenizer_create_char": (_I, [_I, _I, _PP]),
     "mq_tokenizer_destroy": (_I, [_P]),
     "mq_tokenizer_encode_batch": (_I, [_P, ctypes.POINTER(ctypes.c_char_p), _I, _I, _P, _P,

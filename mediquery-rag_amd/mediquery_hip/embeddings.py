@@ -11,13 +11,18 @@ Same contract as LangChain's Embeddings: lists of python floats, one unit-norm
 768-vector per text.  The forward runs in libmqhip.so (HIP, gfx950); nothing here
 computes embeddings on the CPU.
 
-Weights and vocabulary are never downloaded.  A real model needs BOTH a local
-safetensors file and its WordPiece vocab, given as arguments or through the
-environment (so the reference's constructor line stays unchanged):
-    MQ_WEIGHTS_PATH=/models/dmeta.safetensors MQ_VOCAB_FILE=/models/vocab.txt
-Seeded random weights with the char tokenizer (tests, benchmarks) must be asked for
-explicitly with `synthetic=True`: a silently random encoder would hand the Retrieve
-node semantically random documents.
+Weights and vocabulary are never downloaded.  They come, in this order, from:
+  1. `weights_path` + `vocab_file` (or $MQ_WEIGHTS_PATH + $MQ_VOCAB_FILE): a local
+     safetensors file with HF BERT names and its vocab.txt;
+  2. `gguf_path` (or $MQ_GGUF_PATH, or a `weights_path` ending in .gguf): a local GGUF file -
+     weights, architecture and WordPiece vocab in one (gguf.py);
+  3. Ollama's local model store: `model` resolved through its manifest to the GGUF blob an
+     earlier `ollama pull` left there ($OLLAMA_MODELS or ~/.ollama/models) - so the
+     reference's unchanged `OllamaEmbeddings(model="shaw/dmeta-embedding-zh")` runs the
+     same model file on the MI355X.
+Otherwise the constructor raises.  Seeded random weights with the char tokenizer (tests,
+benchmarks) must be asked for explicitly with `synthetic=True`: a silently random encoder
+would hand the Retrieve node semantically random documents.
 """
 import os
 
@@ -25,57 +30,82 @@ import numpy as np
 
 from .compat import EmbeddingsBase
 from .config import BertConfig, DMETA_BASE
+from .gguf import bert_from_gguf, resolve_ollama_model
 from .native import Encoder
 from .tokenizer import NativeTokenizer
 from .weights import load_safetensors
 
 ENV_WEIGHTS = "MQ_WEIGHTS_PATH"
 ENV_VOCAB = "MQ_VOCAB_FILE"
+ENV_GGUF = "MQ_GGUF_PATH"
 
 
 class HipBertEmbeddings(EmbeddingsBase):
     """BERT-base CLS embeddings computed by the hand-written HIP encoder.
 
-    model:        kept for signature parity with OllamaEmbeddings (informational).
-    weights_path: local safetensors with HF BERT names (default: $MQ_WEIGHTS_PATH).
+    model:        the Ollama model name; resolved in Ollama's local store when no weight
+                  file is given (source 3 above).
+    weights_path: local safetensors with HF BERT names (default: $MQ_WEIGHTS_PATH), or a
+                  .gguf file.
     vocab_file:   local WordPiece vocab.txt (default: $MQ_VOCAB_FILE); required with
-                  real weights - the char tokenizer would feed them meaningless ids.
+                  safetensors weights - the char tokenizer would feed them meaningless ids.
+    gguf_path:    local GGUF model file (default: $MQ_GGUF_PATH): weights, config (GELU =
+                  tanh, llama.cpp's) and vocab; `config` overrides the derived config.
     synthetic:    True = seeded random weights + the deterministic char tokenizer
                   (`seed`); the only way to get them.
     """
 
     def __init__(self, model="shaw/dmeta-embedding-zh", *, weights_path=None, vocab_file=None,
-                 synthetic=False, config: BertConfig = DMETA_BASE, seed=0, device=0,
+                 gguf_path=None, synthetic=False, config: BertConfig = None, seed=0, device=0,
                  batch_size=256, max_length=512, **kwargs):
         self.model = model
-        self.config = config
         self.device = device
         self.batch_size = int(batch_size)
-        self.max_length = min(int(max_length), config.max_positions)
         self.synthetic = bool(synthetic)
+        vocab_tokens = None
         if self.synthetic:
-            if weights_path or vocab_file:
-                raise ValueError("synthetic=True takes no weights_path / vocab_file")
+            if weights_path or vocab_file or gguf_path:
+                raise ValueError("synthetic=True takes no weights_path / vocab_file / gguf_path")
+            config = config or DMETA_BASE
             weights = None
         else:
             weights_path = weights_path or os.environ.get(ENV_WEIGHTS)
             vocab_file = vocab_file or os.environ.get(ENV_VOCAB)
-            if not weights_path or not vocab_file:
-                raise ValueError(
-                    "HipBertEmbeddings(model=%r) needs the model's local weights AND vocab "
-                    "(weights_path=/vocab_file= or $%s/$%s; nothing is downloaded). Missing: %s. "
-                    "Pass synthetic=True for seeded random weights (tests/benchmarks only)."
-                    % (model, ENV_WEIGHTS, ENV_VOCAB,
-                       ", ".join(n for n, v in (("weights", weights_path), ("vocab", vocab_file))
-                                 if not v)))
-            for what, p in (("weights", weights_path), ("vocab", vocab_file)):
-                if not os.path.isfile(p):
-                    raise FileNotFoundError("%s file %r does not exist" % (what, p))
-            weights = load_safetensors(weights_path, config)
-        self.weights_path, self.vocab_file = weights_path, vocab_file
+            if weights_path and str(weights_path).endswith(".gguf"):
+                gguf_path, weights_path = weights_path, None
+            gguf_path = gguf_path or (None if weights_path else os.environ.get(ENV_GGUF))
+            if not weights_path and not gguf_path:
+                gguf_path = resolve_ollama_model(model)
+            if gguf_path:
+                if not os.path.isfile(gguf_path):
+                    raise FileNotFoundError("GGUF file %r does not exist" % gguf_path)
+                weights, gcfg, vocab_tokens = bert_from_gguf(gguf_path)
+                config = config or gcfg
+                if vocab_tokens is None and not vocab_file:
+                    raise ValueError("GGUF file %r embeds no BERT vocabulary; pass vocab_file" % gguf_path)
+            else:
+                if not weights_path or not vocab_file:
+                    raise ValueError(
+                        "HipBertEmbeddings(model=%r) needs the model's local files (nothing is "
+                        "downloaded): weights_path= + vocab_file= (or $%s + $%s), gguf_path= (or $%s), "
+                        "or the model pulled into Ollama's local store. Missing: %s. Pass "
+                        "synthetic=True for seeded random weights (tests/benchmarks only)."
+                        % (model, ENV_WEIGHTS, ENV_VOCAB, ENV_GGUF,
+                           ", ".join(n for n, v in (("weights", weights_path), ("vocab", vocab_file))
+                                     if not v)))
+                for what, p in (("weights", weights_path), ("vocab", vocab_file)):
+                    if not os.path.isfile(p):
+                        raise FileNotFoundError("%s file %r does not exist" % (what, p))
+                config = config or DMETA_BASE
+                weights = load_safetensors(weights_path, config)
+        self.config = config
+        self.max_length = min(int(max_length), config.max_positions)
+        self.weights_path, self.vocab_file, self.gguf_path = weights_path, vocab_file, gguf_path
         self.encoder = Encoder(config, weights=weights, seed=seed, device=device)
         if vocab_file:  # C++ tokenizers of libmqhip.so
             self.tokenizer = NativeTokenizer.wordpiece(vocab_file, max_length=self.max_length)
+        elif vocab_tokens is not None:
+            self.tokenizer = NativeTokenizer.wordpiece_tokens(vocab_tokens, max_length=self.max_length)
         else:
             self.tokenizer = NativeTokenizer.char(config.vocab_size, max_length=self.max_length)
 

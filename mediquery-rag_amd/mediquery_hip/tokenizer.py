@@ -158,6 +158,19 @@ class NativeTokenizer:
                   max_length, ctypes.byref(h))
         return cls(h, max_length)
 
+    @classmethod
+    def wordpiece_tokens(cls, tokens, max_length=512, lower_case=True):
+        """WordPiece over an in-memory vocabulary (token of id i = tokens[i]), e.g. the
+        vocab a GGUF model file embeds (gguf.read_gguf)."""
+        import ctypes
+        from . import _lib
+        tokens = list(tokens)
+        arr = (ctypes.c_char_p * len(tokens))(*[t.encode("utf-8") for t in tokens])
+        h = ctypes.c_void_p()
+        _lib.call("mq_tokenizer_create_wordpiece_tokens", arr, len(tokens), int(lower_case), max_length,
+                  ctypes.byref(h))
+        return cls(h, max_length)
+
     def close(self):
         h, self._h = getattr(self, "_h", None), None
         if h:

@@ -73,6 +73,8 @@ def test_embeddings_refuse_silent_synthetic(tmp_path, monkeypatch):
     from mediquery_hip.embeddings import ENV_VOCAB, ENV_WEIGHTS, HipBertEmbeddings
     monkeypatch.delenv(ENV_WEIGHTS, raising=False)
     monkeypatch.delenv(ENV_VOCAB, raising=False)
+    monkeypatch.delenv("MQ_GGUF_PATH", raising=False)
+    monkeypatch.setenv("OLLAMA_MODELS", str(tmp_path / "no_ollama_store"))
     with pytest.raises(ValueError, match="synthetic=True"):
         HipBertEmbeddings(model="shaw/dmeta-embedding-zh")
     w = tmp_path / "w.safetensors"
