@@ -42,7 +42,8 @@ from mediquery_hip import _lib  # noqa: E402
 # scan ("f32_direct_search") and the all-split-f32 variant.
 PRECISIONS = {"f32": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32_SCREEN),
               "f32_direct_search": (_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32),
-              "f32x6": (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32X6)}
+              "f32x6": (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32X6),
+              "f32x6_screen": (_lib.MQ_DTYPE_F32X6, _lib.MQ_DTYPE_F32_SCREEN)}
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
@@ -355,6 +356,7 @@ def main():
     main_r = summarize("f32", runs["f32"])
     direct_r = summarize("f32_direct_search", runs["f32_direct_search"])
     alt_r = summarize("f32x6", runs["f32x6"])
+    alt_s = summarize("f32x6_screen", runs["f32x6_screen"])
     out = {
         "metric": "queries/s (embed+top-k, k=5, b=256) over 1M×768 corpus; p50 single-query ms",
         "value": main_r["value"], "unit": "queries/s", "n_gpus": world, "steps": args.steps,
@@ -382,6 +384,9 @@ def main():
                                                           "search_roofline", "planted_top1_ok")},
         "split_f32": dict(alt_r, dtype="f32 via exact 3-way bf16 split (6 bf16 MFMAs / product, "
                                        "fp32 accumulate); same parity tolerances as f32"),
+        "split_f32_encoder_screened_search": {
+            kk: alt_s[kk] for kk in ("value", "ms_per_step", "encoder_ms", "search_ms", "roofline",
+                                     "planted_top1_ok", "screen_fallbacks", "screen_passdowns")},
     }
     out["config5_bf16_rerank"] = cfg5
     out["secondary_long_queries"] = sec
