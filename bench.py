@@ -158,7 +158,7 @@ def main():
         if ev:
             ev[1].record()
         if world > 1:
-            s, i = searcher.search_local_batch(q, K)
+            s, i = searcher.search_local_batch(q, K, sizes=[B] * world)  # equal batches: no size exchange
         else:
             s, i = local_search(q, K)
         if ev:

@@ -872,9 +872,10 @@ void launch_search(const mq_index* ix, const float* q, int nq, int k, int G, int
 template <int KC, typename IdIn>
 void launch_merge(const float* cs, const IdIn* ci, int n_lists, int64_t nq, int k_in, int k_out,
                   float* os, int64_t* oi, int list_kc, int* overflow, hipStream_t s) {
-  // k_out <= 16: register thread lists (25 us at B = 256); larger k_out: the threshold
-  // merge (k_out = 64: 38 us vs 96 us with 16-entry thread lists + overflow check)
-  if (k_out <= 16)
+  // k_out <= 16 over a batch: register thread lists (25 us at B = 256); larger k_out or
+  // a few queries: the threshold merge (k_out = 64: 38 us vs 96 us with 16-entry thread
+  // lists + overflow check; one query's 512 stream lists, k_out = 16: 29 vs 48 us)
+  if (k_out <= 16 && nq > 32)
     hipLaunchKernelGGL((merge_kernel<KC, IdIn>), dim3((unsigned)nq), dim3(256), 0, s, cs, ci,
                        n_lists, nq, k_in, k_out, os, oi, list_kc, overflow);
   else
@@ -1178,10 +1179,13 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   const bool bf = tier != TIER_X6;
   // candidates: the bf16 screen's error bound is ~3.5e-3 for unit vectors, so it keeps
   // a wide margin - 64 per query in batches (the k-th and 64-th scores of 1M random-ish
-  // rows are ~0.02 apart), max(32, k + 16) for a few streamed queries; the split-f32
-  // screen (bound 8e-5) keeps k + 3 while that fits its 8-entry lists (k <= 5), else k + 8
+  // rows are ~0.02 apart).  Streamed queries keep the fp32 query (bound ~2e-3): 16 for
+  // k <= 5 - exactly the stream kernel's 16-entry lists, so the scan needs no overflow
+  // check and its host round trip (single-query latency) - else max(32, k + 16).  The
+  // split-f32 screen (bound 8e-5) keeps k + 3 while that fits its 8-entry lists (k <= 5),
+  // else k + 8
   const int want = tier == TIER_BF16 ? MQ_MAX_K
-                   : tier == TIER_BF16_STREAM ? std::min(std::max(32, k + 16), MQ_MAX_K)
+                   : tier == TIER_BF16_STREAM ? (k + 11 <= 16 ? 16 : std::min(std::max(32, k + 16), MQ_MAX_K))
                    : (k + 3 <= 8 ? 8 : k + 8);
   const int kc = (int)std::min<int64_t>(want, ix->n);
   int rc = bf ? ensure_shadow(ix, s) : MQ_OK;

@@ -68,15 +68,19 @@ class ShardedSearcher:
         os_, oi = merge_topk_host(gs.numpy(), gi.numpy(), k)
         return torch.from_numpy(os_), torch.from_numpy(oi)
 
-    def search_local_batch(self, q_local, k):
+    def search_local_batch(self, q_local, k, sizes=None):
         """DP-encoded queries: gather every rank's batch, search all, keep own rows.
         Ranks may hold different batch sizes (a ragged last batch): the sizes are
-        all-gathered first, every batch is padded to the largest for the one query
-        all-gather, and the padding is dropped before the scan."""
+        all-gathered first (skipped when the caller passes every rank's `sizes`), every
+        batch is padded to the largest for the one query all-gather, and the padding is
+        dropped before the scan."""
         rank = dist.get_rank(self.group)
         B = int(q_local.shape[0])
-        sizes = self._all_gather(torch.tensor([B], dtype=torch.int64, device=q_local.device))
-        sizes = [int(x) for x in sizes.reshape(-1).tolist()]
+        if sizes is None:
+            sizes = self._all_gather(torch.tensor([B], dtype=torch.int64, device=q_local.device))
+            sizes = [int(x) for x in sizes.reshape(-1).tolist()]
+        elif len(sizes) != dist.get_world_size(self.group) or sizes[rank] != B:
+            raise ValueError("sizes %s do not match world size / this rank's batch %d" % (sizes, B))
         Bmax = max(sizes)
         if Bmax != B:
             pad = torch.zeros((Bmax - B, q_local.shape[1]), dtype=q_local.dtype, device=q_local.device)
