@@ -362,64 +362,6 @@ __global__ __launch_bounds__(256) void scatter_results_kernel(const float* __res
   oi[idx[j] * k + c] = si[t];
 }
 
-// Exact fp32 re-rank of the coarse candidates: one block per query, one wave per
-// candidate dot product (768-wide, float4 per lane), then every candidate's rank by
-// (score desc, id asc) picks its output slot.
-__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q,
-                                                     const float* __restrict__ rows, int dim,
-                                                     const int64_t* __restrict__ cand, int kc,
-                                                     int k, float* __restrict__ out_s,
-                                                     int64_t* __restrict__ out_i) {
-  __shared__ float sc[MQ_MAX_K];
-  __shared__ long long sid[MQ_MAX_K];
-  const int64_t q = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  // eight candidates per wave per round, their row loads in flight together (the
-  // gathered rows come from HBM: the round is latency-bound, so more in flight per lane)
-  constexpr int U = 8;
-  for (int c0 = wave * U; c0 < kc; c0 += 4 * U) {
-    long long id[U];
-    float acc[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      id[u] = c0 + u < kc ? cand[q * kc + c0 + u] : -1;
-      acc[u] = 0.f;
-    }
-    for (int i = lane; i < dim / 4; i += 64) {
-      const floatx4 a = q4[i];
-      floatx4 b[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
-      if (lane == 0 && c0 + u < kc) {
-        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
-        sid[c0 + u] = id[u];
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < kc) {
-    int rank = 0;
-    for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
-    if (rank < k) {
-      out_s[q * k + rank] = sid[tid] >= 0 ? sc[tid] : -INFINITY;
-      out_i[q * k + rank] = sid[tid];
-    }
-  } else if (tid < k) {
-    out_s[q * k + tid] = -INFINITY;  // k > kc: padding past the candidates
-    out_i[q * k + tid] = -1;
-  }
-}
-
 // Certificate of the screened exact search (MQ_DTYPE_F32_SCREEN).  A screen scan kept
 // the kc best rows of each query by its approximate score s, so a row r outside them
 // has s_r <= s_kc; if every s is within E of the exact dot e, and e_k (the fp32 re-rank
@@ -436,17 +378,14 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
 // A query that fails is appended to fail[] (count in *n_fail) and re-run one tier down.
 // One wave per query.
 enum { VERIFY_X6 = 0, VERIFY_BF16_Q16 = 1, VERIFY_BF16_Q32 = 2 };
+constexpr int kNoPrune = -1;
 
-__global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restrict__ Q, int dim,
-                                                            const float* __restrict__ cs, int kc,
-                                                            const float* __restrict__ es, int k,
-                                                            int64_t nq, int mode,
-                                                            const unsigned* __restrict__ stats,
-                                                            int* __restrict__ n_fail,
-                                                            int64_t* __restrict__ fail) {
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= nq) return;
+// The screen's bound E on |screen score - exact fp32 dot| for query q (per mode, above),
+// from wave-reduced ||q||^2, ||q - bq||^2, ||bq||^2 (Q16: bq = q rounded as
+// to_bf16_kernel does).  Evaluated by one full wave; every lane returns E.
+__device__ __forceinline__ float screen_bound(const float* __restrict__ Q, int dim, int64_t q,
+                                              int mode, const unsigned* __restrict__ stats,
+                                              int lane) {
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
   float ss = 0.f, sd = 0.f, sb = 0.f;
   for (int i = lane; i < (dim >> 2); i += 64) {
@@ -466,20 +405,112 @@ __global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restr
     sd += __shfl_xor(sd, off);
     sb += __shfl_xor(sb, off);
   }
-  if (lane != 0) return;
   const float qn = sqrtf(ss);
-  float E;
-  if (mode == VERIFY_X6) {
-    E = 8e-5f * qn;
-  } else {
-    // 1.001: slack for the fp32 evaluation of the norms and of this bound
-    const float dmax = __uint_as_float(stats[0]) * 1.001f, cmax = __uint_as_float(stats[1]) * 1.001f;
-    const float g = 2.f * (float)dim * 5.9604645e-8f;
-    const float dq = mode == VERIFY_BF16_Q16 ? sqrtf(sd) : 0.f;
-    const float bqn = mode == VERIFY_BF16_Q16 ? sqrtf(sb) : qn;
-    E = (dq * cmax + bqn * dmax + g * bqn * (cmax + dmax) + g * qn * cmax) * 1.001f + 1e-7f;
-  }
+  if (mode == VERIFY_X6) return 8e-5f * qn;
+  // 1.001: slack for the fp32 evaluation of the norms and of this bound
+  const float dmax = __uint_as_float(stats[0]) * 1.001f, cmax = __uint_as_float(stats[1]) * 1.001f;
+  const float g = 2.f * (float)dim * 5.9604645e-8f;
+  const float dq = mode == VERIFY_BF16_Q16 ? sqrtf(sd) : 0.f;
+  const float bqn = mode == VERIFY_BF16_Q16 ? sqrtf(sb) : qn;
+  return (dq * cmax + bqn * dmax + g * bqn * (cmax + dmax) + g * qn * cmax) * 1.001f + 1e-7f;
+}
+
+__global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restrict__ Q, int dim,
+                                                            const float* __restrict__ cs, int kc,
+                                                            const float* __restrict__ es, int k,
+                                                            int64_t nq, int mode,
+                                                            const unsigned* __restrict__ stats,
+                                                            int* __restrict__ n_fail,
+                                                            int64_t* __restrict__ fail) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const float E = screen_bound(Q, dim, q, mode, stats, lane);
+  if (lane != 0) return;
   if (!(cs[q * kc + kc - 1] + E < es[q * k + k - 1])) fail[atomicAdd(n_fail, 1)] = q;
+}
+
+// Exact fp32 re-rank of the coarse candidates: one block per query, one wave per
+// candidate dot product (768-wide, float4 per lane), then every candidate's rank by
+// (score desc, id asc) picks its output slot.
+// prune_mode (a VERIFY_* mode, or kNoPrune): with screen scores cs (sorted desc) and the
+// screen's bound E, a candidate with cs < cs_k - 2E cannot be in the exact top-k (the k
+// best screen scores are exact >= cs_k - E each, it is exact <= cs + E), so only the
+// prefix cs >= cs_k - 2E is gathered and dotted (typically a handful of 64).
+__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q,
+                                                     const float* __restrict__ rows, int dim,
+                                                     const int64_t* __restrict__ cand, int kc,
+                                                     int k, float* __restrict__ out_s,
+                                                     int64_t* __restrict__ out_i,
+                                                     const float* __restrict__ cs, int prune_mode,
+                                                     const unsigned* __restrict__ stats) {
+  __shared__ float sc[MQ_MAX_K];
+  __shared__ long long sid[MQ_MAX_K];
+  __shared__ int n_live;
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
+  if (tid < kc) {
+    sc[tid] = -INFINITY;
+    sid[tid] = -1;
+  }
+  if (wave == 0) {
+    int live = kc;
+    if (prune_mode != kNoPrune && k < kc) {
+      const float E = screen_bound(Q, dim, q, prune_mode, stats, lane);
+      const float cut = cs[q * kc + k - 1] - 2.f * E;
+      // candidates are sorted by screen score: the live ones are a prefix
+      const bool keep = lane < kc && !(cs[q * kc + lane] < cut);
+      live = __popcll(__ballot(keep)) + (kc > 64 ? kc - 64 : 0);
+      live = max(live, k);
+    }
+    if (lane == 0) n_live = live;
+  }
+  __syncthreads();
+  const int kl = n_live;
+  // eight candidates per wave per round, their row loads in flight together (the
+  // gathered rows come from HBM: the round is latency-bound, so more in flight per lane)
+  constexpr int U = 8;
+  for (int c0 = wave * U; c0 < kl; c0 += 4 * U) {
+    long long id[U];
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      id[u] = c0 + u < kl ? cand[q * kc + c0 + u] : -1;
+      acc[u] = 0.f;
+    }
+    for (int i = lane; i < dim / 4; i += 64) {
+      const floatx4 a = q4[i];
+      floatx4 b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
+      if (lane == 0 && c0 + u < kl) {
+        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
+        sid[c0 + u] = id[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < kc) {
+    int rank = 0;
+    for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
+    if (rank < k) {
+      out_s[q * k + rank] = sid[tid] >= 0 ? sc[tid] : -INFINITY;
+      out_i[q * k + rank] = sid[tid];
+    }
+  } else if (tid < k) {
+    out_s[q * k + tid] = -INFINITY;  // k > kc: padding past the candidates
+    out_i[q * k + tid] = -1;
+  }
 }
 
 // ======================================================= K10: merge lists ======
@@ -1143,7 +1174,7 @@ int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* o
                                 ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
-                     ix->coarse_i.as<int64_t>(), kc, k, os, oi);
+                     ix->coarse_i.as<int64_t>(), kc, k, os, oi, nullptr, kNoPrune, nullptr);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1200,16 +1231,17 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   rc = kind == SCAN_BF16 ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
                          : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
+  const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
+  const unsigned* stats = bf ? ix->stats16.as<unsigned>() : nullptr;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
-                     ix->coarse_i.as<int64_t>(), kc, k, os, oi);
+                     ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), mode, stats);
   MQ_HIP(hipGetLastError());
   if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
   int64_t* fail = ix->tier_fail[tier].as<int64_t>();
   MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
-  const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
   hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
-                     ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode,
-                     bf ? ix->stats16.as<unsigned>() : nullptr, ix->flag.as<int>(), fail);
+                     ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
+                     fail);
   MQ_HIP(hipGetLastError());
   int n_fail = 0;
   MQ_HIP(hipMemcpyAsync(&n_fail, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -42,7 +42,7 @@ constexpr int kTsRank = 8;       // tau = 8th largest list maximum of the sample
 
 enum { TS_MAX = 0, TS_APPEND = 1 };
 
-constexpr int kTsWaveSurv = 96;  // LDS survivor slots per wave (TS_APPEND)
+constexpr int kTsWaveSurv = 160;  // LDS survivor slots per wave (TS_APPEND; fills the 160 KB with NCH 12)
 struct Survivor {
   float s;
   int row;
@@ -305,8 +305,12 @@ __global__ __launch_bounds__(256) void bf16_select_kernel(const float* __restric
 
 template <int NCH>
 void launch_nch(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
-  const int G = a.num_cus;
+  // One workgroup per CU in total (LDS and VGPRs allow one): several query groups split
+  // the CUs instead of running in rounds.  G is a multiple of the 8 XCDs, so (x, y) and
+  // (x, y') sit on one XCD and stream the same blocks at about the same time through its
+  // L2 - one HBM read serves every group.
   const int gy = (a.nq + kTsQ - 1) / kTsQ;
+  const int G = gy == 1 ? a.num_cus : std::max(8, a.num_cus / gy / 8 * 8);
   const int64_t n_blocks = (a.n + kTsRows - 1) / kTsRows;
   const uint4* qb = reinterpret_cast<const uint4*>(a.q16);
   tl->mark(s, 0);
