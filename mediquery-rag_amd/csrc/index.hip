@@ -736,20 +736,23 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
       if ((long long)ci[off] >= 0) key[j] = score_key(cs[off]);
     }
   }
+  // Per wave: Tw = the largest key with at least k_out of the WAVE's heads >= Tw (bitwise
+  // search, ballot counts, no block barrier); T = max over the 4 waves still has k_out
+  // heads >= T (all in one wave), so it is a valid threshold - at most ~4x more
+  // survivors than the block-wide k_out-th head, for 62 fewer barriers.
+  const int jn = min(kSelHeads, (n_lists + 255) / 256);  // head slots in use
   unsigned T = 0;
   for (int b = 31; b >= 0; --b) {
     const unsigned cand = T | (1u << b);
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < kSelHeads; ++j) c += key[j] >= cand ? 1 : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    if (lane == 0) part[wave] = c;
-    __syncthreads();
-    const int tot = part[0] + part[1] + part[2] + part[3];
-    __syncthreads();
-    if (tot >= k_out) T = cand;
+    for (int j = 0; j < kSelHeads; ++j)
+      if (j < jn) c += __popcll(__ballot(key[j] >= cand));  // jn is block-uniform
+    if (c >= k_out) T = cand;
   }
+  if (lane == 0) part[wave] = (int)T;
+  __syncthreads();
+  T = max(max((unsigned)part[0], (unsigned)part[1]), max((unsigned)part[2], (unsigned)part[3]));
   const unsigned adm = T > 1u ? T : 1u;  // fewer than k_out valid heads: every valid entry
   if (tid == 0) {
     n_s = 0;
