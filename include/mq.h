@@ -114,12 +114,19 @@ int mq_index_set_stream_threshold(mq_index* ix, int max_queries);
  * it -> top-kc of the survivors), 0 = the tiled scan with per-lane lists + merge.
  * Same candidates either way up to bf16-score ties at the kc-th place. */
 int mq_index_set_threshold_scan(mq_index* ix, int enabled);
+/* Single-query MQ_DTYPE_F32_SCREEN searches over >= 65536 rows of dim 256/512/768/1024:
+ * 1 (default) = screen on an int8 shadow first (one byte per element + a per-row scale,
+ * threshold scan for 64 candidates, fp32 re-rank, certificate with the int8 shadow's
+ * measured error bound); uncertified queries re-run on the bf16 stream tier, and after a
+ * run of failures (a corpus whose top scores crowd within the int8 bound) the int8 tier
+ * sits out the next 256 searches.  0 = start at the bf16 stream tier.  Same results. */
+int mq_index_set_int8_screen(mq_index* ix, int enabled);
 /* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
  * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
 /* Screen counters (MQ_DTYPE_F32_SCREEN; either pointer may be NULL): queries whose
- * certificates failed and that were re-run on the direct exact scan, and bf16-screened
- * queries re-run on the split-f32 screen. */
+ * certificates failed and that were re-run on the direct exact scan, and queries passed
+ * down to the next screen (bf16 batch -> split-f32, int8 single -> bf16 stream). */
 int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
@@ -211,6 +218,12 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
  * kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
+
+/* The int8 screen (K9q) alone for one host query: its kc candidates (screen scores
+ * desc, ids; slots past the survivors hold (tau, -1)) and the int8 shadow's statistics
+ * stats[0] = max ||c - scale r8||, stats[1] = max ||scale r8||.  For kernel unit tests. */
+int mq_debug_int8_screen(mq_index* ix, const float* query, int kc, float* out_scores, int64_t* out_ids,
+                         float* stats);
 
 #ifdef __cplusplus
 }

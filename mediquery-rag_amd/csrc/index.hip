@@ -878,14 +878,19 @@ struct mq_index {
   DevBuf stats16;    // shadow rounding maxima: [0] max ||c - bf16(c)||, [1] max ||c|| (float bits)
   DevBuf q16, coarse_s, coarse_i;
   DevBuf flag;          // merge overflow flag (k > 16) / screen failure count
-  DevBuf tier_fail[3], tier_q[3], tier_s[3], tier_i[3];  // per screen tier: re-run subset
+  DevBuf tier_fail[4], tier_q[4], tier_s[4], tier_i[4];  // per screen tier: re-run subset
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
   int64_t remerges = 0;  // merges re-run with 64-entry thread lists
   int64_t screen_fallbacks = 0;  // screened queries re-run on the direct exact scan
   int64_t screen_passdowns = 0;  // bf16-screened queries re-run on the split-f32 screen
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   bool thresh_scan = true;  // batched bf16 screens use the threshold scan (K9t)
-  DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t: sample maxima, tau, survivors
+  DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t / K9q: sample maxima, tau, survivors
+  DevBuf rows8, scale8, stats8;  // int8 shadow [cap, dim] + per-row scales + its maxima (as stats16)
+  int64_t n8 = 0;                // rows already mirrored into rows8
+  bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
+  double i8_fail_avg = 0.0;      // running share of single queries the int8 screen failed to certify
+  int i8_skip = 0;               // searches left that bypass the int8 tier after a bad run
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -1156,6 +1161,55 @@ int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, i
   return MQ_OK;
 }
 
+// int8 shadow (K9q) of the stored rows, extended lazily like the bf16 one.
+int ensure_i8(mq_index* ix, hipStream_t s) {
+  int rc = ix->rows8.ensure((size_t)(ix->cap + kI8PadRows) * ix->dim);
+  if (!rc) rc = ix->scale8.ensure((size_t)(ix->cap + kI8PadRows) * sizeof(float));
+  if (!rc) rc = ix->stats8.ensure(2 * sizeof(unsigned));
+  if (rc) return rc;
+  if (ix->n8 < ix->n) {
+    if (ix->n8 == 0) MQ_HIP(hipMemsetAsync(ix->stats8.p, 0, 2 * sizeof(unsigned), s));
+    launch_i8_shadow(ix->rows + ix->n8 * ix->dim, ix->n - ix->n8, ix->dim,
+                     ix->rows8.as<unsigned>() + ix->n8 * ix->dim / 4, ix->scale8.as<float>() + ix->n8,
+                     ix->stats8.as<unsigned>(), s);
+    MQ_HIP(hipGetLastError());
+    ix->n8 = ix->n;
+  }
+  return MQ_OK;
+}
+
+// The int8 screen applies to one query over >= kTsMinRows rows of dim 256..1024, unless
+// it failed to certify most recent queries (then it sits out i8_skip searches).
+bool i8_ok(mq_index* ix, int64_t nq) {
+  if (!ix->i8_screen || nq != 1 || ix->dim % 256 != 0 || ix->dim > 1024 || ix->n < kTsMinRows ||
+      ix->n >= (1ll << 31))
+    return false;
+  if (ix->i8_skip > 0) {
+    --ix->i8_skip;
+    return false;
+  }
+  return true;
+}
+
+int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t* oi, hipStream_t s) {
+  const size_t n_lists = (size_t)i8_lists(ix->num_cus);
+  int rc = ensure_i8(ix, s);
+  if (!rc) rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
+  if (!rc) rc = ix->ts_tau.ensure(nq * sizeof(float));
+  if (!rc) rc = ix->ts_count.ensure(nq * sizeof(int));
+  if (!rc) rc = ix->ts_cs.ensure((size_t)nq * kTsCap * sizeof(float));
+  if (!rc) rc = ix->ts_ci.ensure((size_t)nq * kTsCap * sizeof(int));
+  if (rc) return rc;
+  ThreshI8Args a{q, (int)nq, ix->rows8.as<unsigned>(), ix->scale8.as<float>(), ix->n, ix->dim, ix->num_cus,
+                 kc, ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
+                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi};
+  if (ix->tl.used > 4096) ix->tl.drain();
+  launch_thresh_i8(a, s, &ix->tl);
+  ix->tl.close(s);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
 // the bf16 candidate scan of a batch: K9t when it applies, else the tiled K9 + K10
 int bf16_candidates(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
                     hipStream_t s) {
@@ -1201,8 +1255,10 @@ int search_direct(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
 //   TIER_BF16         batches: bf16 MFMA scan of the shadow -> split-f32 tier (> 64
 //                     failing queries) or the direct exact scan
 //   TIER_X6           split-f32 MFMA scan -> direct exact scan
+//   TIER_I8           one query: int8 shadow threshold scan (K9q, a quarter of the fp32
+//                     bytes) for 64 candidates -> TIER_BF16_STREAM
 // Synchronous (reads the failure count).
-enum ScreenTier { TIER_BF16_STREAM = 0, TIER_BF16 = 1, TIER_X6 = 2 };
+enum ScreenTier { TIER_BF16_STREAM = 0, TIER_BF16 = 1, TIER_X6 = 2, TIER_I8 = 3 };
 
 bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
   return nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024;
@@ -1210,7 +1266,7 @@ bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
 
 int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, float* os,
                     int64_t* oi, hipStream_t s) {
-  const bool bf = tier != TIER_X6;
+  const bool bf = tier == TIER_BF16_STREAM || tier == TIER_BF16;
   // candidates: the bf16 screen's error bound is ~3.5e-3 for unit vectors, so it keeps
   // a wide margin - 64 per query in batches (the k-th and 64-th scores of 1M random-ish
   // rows are ~0.02 apart).  Streamed queries keep the fp32 query (bound ~2e-3): 16 for
@@ -1218,7 +1274,7 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   // check and its host round trip (single-query latency) - else max(32, k + 16).  The
   // split-f32 screen (bound 8e-5) keeps k + 3 while that fits its 8-entry lists (k <= 5),
   // else k + 8
-  const int want = tier == TIER_BF16 ? MQ_MAX_K
+  const int want = tier == TIER_BF16 || tier == TIER_I8 ? MQ_MAX_K
                    : tier == TIER_BF16_STREAM ? (k + 11 <= 16 ? 16 : std::min(std::max(32, k + 16), MQ_MAX_K))
                    : (k + 3 <= 8 ? 8 : k + 8);
   const int kc = (int)std::min<int64_t>(want, ix->n);
@@ -1231,11 +1287,14 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   if (rc) return rc;
   const int kind = tier == TIER_X6 ? SCAN_X6 : tier == TIER_BF16 ? SCAN_BF16 : SCAN_STREAM16;
   const float* qs = tier == TIER_BF16 ? ix->q16.as<float>() : q;
-  rc = kind == SCAN_BF16 ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
-                         : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
+  rc = tier == TIER_I8 ? i8_topk(ix, q, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
+       : kind == SCAN_BF16
+           ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
+           : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
   if (rc) return rc;
+  // the int8 screen's bound has the Q32 form (fp32 query) with the int8 shadow's maxima
   const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
-  const unsigned* stats = bf ? ix->stats16.as<unsigned>() : nullptr;
+  const unsigned* stats = bf ? ix->stats16.as<unsigned>() : tier == TIER_I8 ? ix->stats8.as<unsigned>() : nullptr;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
                      ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), mode, stats);
   MQ_HIP(hipGetLastError());
@@ -1249,6 +1308,15 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   int n_fail = 0;
   MQ_HIP(hipMemcpyAsync(&n_fail, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
+  if (tier == TIER_I8) {
+    // a corpus whose top scores crowd within the int8 bound fails most certificates: after
+    // a run of failures the single-query path goes straight to the bf16 stream for a while
+    ix->i8_fail_avg = 0.9 * ix->i8_fail_avg + 0.1 * (double)n_fail / (double)nq;
+    if (ix->i8_fail_avg > 0.3) {
+      ix->i8_skip = 256;
+      ix->i8_fail_avg = 0.0;
+    }
+  }
   if (n_fail == 0) return MQ_OK;
   // re-run the uncertified queries one tier down, into this tier's scratch
   rc = ix->tier_q[tier].ensure((size_t)n_fail * ix->dim * sizeof(float));
@@ -1264,6 +1332,9 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   if (tier == TIER_BF16 && x6_tier_ok(ix, n_fail, k)) {
     ix->screen_passdowns += n_fail;
     rc = search_screened(ix, TIER_X6, sq, n_fail, k, ss, si, s);
+  } else if (tier == TIER_I8) {
+    ix->screen_passdowns += n_fail;
+    rc = search_screened(ix, TIER_BF16_STREAM, sq, n_fail, k, ss, si, s);
   } else {
     ix->screen_fallbacks += n_fail;
     rc = search_direct(ix, sq, n_fail, k, ss, si, s);
@@ -1283,6 +1354,7 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
   const bool screen = ix->precision == MQ_DTYPE_F32_SCREEN;
   if (nq <= ix->stream_max_q && stream_ok(ix)) {  // few queries: streaming scans
+    if (screen && i8_ok(ix, nq)) return search_screened(ix, TIER_I8, q, nq, k, os, oi, s);
     if (screen && ix->dim % 128 == 0) return search_screened(ix, TIER_BF16_STREAM, q, nq, k, os, oi, s);
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   }
@@ -1308,7 +1380,8 @@ int reserve_rows(mq_index* ix, int64_t need_rows, hipStream_t s) {
   if (ix->rows) MQ_HIP(hipFree(ix->rows));
   ix->rows = fresh;
   ix->cap = new_cap;
-  ix->n16 = 0;  // the bf16 shadow is rebuilt at the next coarse search
+  ix->n16 = 0;  // the bf16 / int8 shadows are rebuilt at the next screened search
+  ix->n8 = 0;
   return MQ_OK;
 }
 
@@ -1368,7 +1441,10 @@ int mq_index_destroy(mq_index* ix) {
     ix->coarse_i.release();
     ix->flag.release();
     ix->stats16.release();
-    for (int t = 0; t < 3; ++t) {
+    for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->rows8,
+                      &ix->scale8, &ix->stats8})
+      b->release();
+    for (int t = 0; t < 4; ++t) {
       ix->tier_fail[t].release();
       ix->tier_q[t].release();
       ix->tier_s[t].release();
@@ -1406,6 +1482,7 @@ int mq_index_reset(mq_index* ix) {
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->n = 0;
   ix->n16 = 0;
+  ix->n8 = 0;
   return MQ_OK;
 }
 
@@ -1483,6 +1560,7 @@ int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst
   dst->cap = n;
   dst->n = n;
   dst->n16 = 0;
+  dst->n8 = 0;
   return MQ_OK;
 }
 
@@ -1508,6 +1586,29 @@ int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k, float
   if (rc) return rc;
   MQ_HIP(hipMemcpyAsync(out_scores, ix->out_s.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
   MQ_HIP(hipMemcpyAsync(out_ids, ix->out_i.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_debug_int8_screen(mq_index* ix, const float* query, int kc, float* out_scores, int64_t* out_ids,
+                         float* stats) {
+  clear_error();
+  MQ_CHECK_ARG(ix && query && out_scores && out_ids && stats, "NULL argument");
+  MQ_CHECK_ARG(kc >= 1 && kc <= MQ_MAX_K, "kc must be in [1, %d]", MQ_MAX_K);
+  MQ_CHECK_ARG(ix->dim % 256 == 0 && ix->dim <= 1024 && ix->n >= 1, "int8 screen needs dim 256..1024, rows");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  hipStream_t s = nullptr;
+  int rc = ix->stage.ensure((size_t)ix->dim * 4);
+  if (!rc) rc = ix->out_s.ensure((size_t)kc * 4);
+  if (!rc) rc = ix->out_i.ensure((size_t)kc * 8);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(ix->stage.p, query, (size_t)ix->dim * 4, hipMemcpyHostToDevice, s));
+  rc = i8_topk(ix, ix->stage.as<float>(), 1, kc, ix->out_s.as<float>(), ix->out_i.as<int64_t>(), s);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(out_scores, ix->out_s.p, (size_t)kc * 4, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(out_ids, ix->out_i.p, (size_t)kc * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(stats, ix->stats8.p, 2 * sizeof(float), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
   return MQ_OK;
 }
@@ -1556,6 +1657,16 @@ int mq_index_set_threshold_scan(mq_index* ix, int enabled) {
   MQ_CHECK_ARG(ix, "NULL index");
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->thresh_scan = enabled != 0;
+  return MQ_OK;
+}
+
+int mq_index_set_int8_screen(mq_index* ix, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->i8_screen = enabled != 0;
+  ix->i8_skip = 0;
+  ix->i8_fail_avg = 0.0;
   return MQ_OK;
 }
 
@@ -1643,6 +1754,7 @@ int mq_index_load(mq_index* ix, const char* path) {
   }
   ix->n = 0;
   ix->n16 = 0;
+  ix->n8 = 0;
   int rc = reserve_rows(ix, h.n_rows, nullptr);
   if (rc) {
     fclose(f);

@@ -335,4 +335,254 @@ void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   }
 }
 
+// ============================ K9q: int8 threshold scan (few-query screens) ==========
+// A single query (or up to 4) over the int8 shadow: a row is stored as int8 r8 with one
+// fp32 scale (absmax / 127), 1 byte per element - half the bytes of the bf16 shadow that
+// bounds the few-query screen (HBM-bound: ~0.13 instead of ~0.24 ms at 1M x 768).  The
+// screen score of row c is fl(scale_c * fl(sum_j q_j r8_cj)) with the fp32 query; its
+// error against the exact dot is bounded as in VERIFY_BF16_Q32 with the int8 shadow's own
+// maxima (dmax = max ||c - scale_c r8_c||, cmax = max ||scale_c r8_c||).  Same threshold
+// scheme as K9t (sample pass -> tau -> appending pass -> select), on the VALU: lane l
+// holds elements [l E, l E + E) of every row (E = dim / 64) and of the query, in
+// registers; a wave takes 8 rows per step (8 x dim bytes, contiguous), converts and
+// multiplies, and one transposed butterfly (xor 32 / 16 / 8 halving the values, then
+// xor 4 / 2 / 1) leaves lane l with row 4 b5 + 2 b4 + b3 of the 8.
+
+// int8 shadow of rows [0, n) + scales + the screen statistics (float bits, atomicMax).
+// One wave per row; lane l quantises elements [l E, l E + E), E = 4 * E4.
+template <int E4>
+__global__ __launch_bounds__(256) void i8_shadow_kernel(const float* __restrict__ src, int64_t n,
+                                                        unsigned* __restrict__ r8,
+                                                        float* __restrict__ scale,
+                                                        unsigned* __restrict__ stats) {
+  constexpr int E = 4 * E4, DIM = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  floatx4 x[E4];
+  float amax = 0.f;
+#pragma unroll
+  for (int d = 0; d < E4; ++d) {
+    x[d] = *reinterpret_cast<const floatx4*>(src + row * DIM + lane * E + 4 * d);
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x[d].x), fabsf(x[d].y)), fmaxf(fabsf(x[d].z), fabsf(x[d].w))));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+  const float sc = amax / 127.f, inv = amax > 0.f ? 127.f / amax : 0.f;
+  float se = 0.f, sd = 0.f;
+#pragma unroll
+  for (int d = 0; d < E4; ++d) {
+    unsigned w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float v = x[d][b];
+      const float r = fminf(fmaxf(rintf(v * inv), -127.f), 127.f);
+      const float deq = sc * r;
+      se += (v - deq) * (v - deq);
+      sd += deq * deq;
+      w |= ((unsigned)(int)r & 0xffu) << (8 * b);
+    }
+    r8[row * (DIM / 4) + lane * E4 + d] = w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    se += __shfl_xor(se, off);
+    sd += __shfl_xor(sd, off);
+  }
+  if (lane == 0) {
+    scale[row] = sc;
+    atomicMax(stats, __float_as_uint(sqrtf(se)));
+    atomicMax(stats + 1, __float_as_uint(sqrtf(sd)));
+  }
+}
+
+constexpr int kI8Rows = 8;  // rows per wave step
+
+// values v[0 .. 8 NQ) indexed r * NQ + q -> lane l holds v[0 .. NQ) of row
+// 4 b5(l) + 2 b4(l) + b3(l), summed over the 64 lanes
+template <int NQ>
+__device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int lane) {
+#pragma unroll
+  for (int m = 32, c = kI8Rows * NQ; m >= 8; m >>= 1, c >>= 1) {
+    const bool hi = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < c / 2; ++i) {
+      const float keep = hi ? v[i + c / 2] : v[i];
+      const float give = hi ? v[i] : v[i + c / 2];
+      v[i] = keep + __shfl_xor(give, m);
+    }
+  }
+#pragma unroll
+  for (int m = 4; m > 0; m >>= 1)
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) v[i] += __shfl_xor(v[i], m);
+}
+
+template <int E4>
+__device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t n_rows, int64_t unit,
+                                        int lane, unsigned (&a)[kI8Rows][E4]) {
+  constexpr int DIM4 = 64 * E4;  // dwords per row (dim = 256 E4 one-byte elements)
+#pragma unroll
+  for (int r = 0; r < kI8Rows; ++r) {
+    const int64_t row = min(unit * kI8Rows + r, n_rows - 1);
+#pragma unroll
+    for (int d = 0; d < E4; ++d) a[r][d] = r8[row * DIM4 + lane * E4 + d];
+  }
+}
+
+template <int E4, int NQ>
+__device__ __forceinline__ void i8_dot(const unsigned (&a)[kI8Rows][E4], const float (&qv)[NQ][4 * E4],
+                                       float (&v)[kI8Rows * NQ]) {
+#pragma unroll
+  for (int r = 0; r < kI8Rows; ++r) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[r * NQ + q] = 0.f;
+#pragma unroll
+    for (int d = 0; d < E4; ++d)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float x = (float)((int)(a[r][d] << (24 - 8 * b)) >> 24);  // signed byte b
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[r * NQ + q] = fmaf(qv[q][4 * d + b], x, v[r * NQ + q]);
+      }
+  }
+}
+
+// MODE TS_MAX: every `period`-th unit, per-workgroup maxima -> lmax[q][workgroup];
+// TS_APPEND: every unit, score >= tau[q] appended to the query's survivors.
+template <int E4, int NQ, int MODE>
+__global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
+    const float* __restrict__ Q, int nq, const unsigned* __restrict__ r8, const float* __restrict__ scale,
+    int64_t n_rows, int64_t n_units, int period, const float* __restrict__ tau, float* __restrict__ lmax,
+    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci) {
+  constexpr int E = 4 * E4, DIM = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int W = gridDim.x * 4;
+  float qv[NQ][E];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const float* src = Q + (int64_t)min(q, nq - 1) * DIM + lane * E;
+#pragma unroll
+    for (int d = 0; d < E4; ++d) {
+      const floatx4 t = *reinterpret_cast<const floatx4*>(src + 4 * d);
+      qv[q][4 * d] = t.x;
+      qv[q][4 * d + 1] = t.y;
+      qv[q][4 * d + 2] = t.z;
+      qv[q][4 * d + 3] = t.w;
+    }
+  }
+  float th[NQ], mx[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    th[q] = MODE == TS_APPEND ? tau[min(q, nq - 1)] : 0.f;
+    mx[q] = -INFINITY;
+  }
+  const int my_r = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+  const int64_t stride = (int64_t)W * period;
+  unsigned a[2][kI8Rows][E4];
+  float sc[2];
+  int64_t u = (int64_t)gw * period;
+  auto fetch = [&](int buf, int64_t unit) {
+    const int64_t uu = min(unit, n_units - 1);  // past the end: re-read the last unit
+    i8_load<E4>(r8, n_rows, uu, lane, a[buf]);
+    sc[buf] = scale[min(uu * kI8Rows + my_r, n_rows - 1)];
+  };
+  auto consume = [&](int buf, int64_t unit) {
+    float v[kI8Rows * NQ];
+    i8_dot<E4, NQ>(a[buf], qv, v);
+    transpose_reduce<NQ>(v, lane);
+    const int64_t row = unit * kI8Rows + my_r;
+    const bool valid = row < n_rows;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float score = v[q] * sc[buf];
+      if (MODE == TS_MAX) {
+        mx[q] = valid ? fmaxf(mx[q], score) : mx[q];
+      } else if ((lane & 7) == 0 && valid && q < nq && score >= th[q]) {
+        const int slot = atomicAdd(count + q, 1);
+        if (slot < kTsCap) {
+          cs[(int64_t)q * kTsCap + slot] = score;
+          ci[(int64_t)q * kTsCap + slot] = (int)row;
+        }
+      }
+    }
+  };
+  if (u < n_units) fetch(0, u);
+  // two register stages: the next unit's loads are in flight while one is multiplied
+  while (u < n_units) {
+    const int64_t u1 = u + stride;
+    fetch(1, u1);
+    consume(0, u);
+    if (u1 >= n_units) break;
+    const int64_t u2 = u1 + stride;
+    fetch(0, u2);
+    consume(1, u1);
+    u = u2;
+  }
+  if (MODE == TS_MAX) {  // workgroup maxima: one list per workgroup (a shorter tau pass)
+    __shared__ float wmax[4][NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float m = mx[q];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+      if (lane == 0) wmax[threadIdx.x >> 6][q] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < NQ && (int)threadIdx.x < nq) {
+      const int q = threadIdx.x;
+      lmax[(int64_t)q * gridDim.x + blockIdx.x] =
+          fmaxf(fmaxf(wmax[0][q], wmax[1][q]), fmaxf(wmax[2][q], wmax[3][q]));
+    }
+  }
+}
+
+template <int E4>
+void i8_shadow_e4(const float* rows, int64_t n, unsigned* r8, float* scale, unsigned* stats, hipStream_t s) {
+  hipLaunchKernelGGL((i8_shadow_kernel<E4>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rows, n, r8,
+                     scale, stats);
+}
+
+void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, unsigned* stats,
+                      hipStream_t s) {
+  switch (dim / 256) {
+    case 1: i8_shadow_e4<1>(rows, n, r8, scale, stats, s); break;
+    case 2: i8_shadow_e4<2>(rows, n, r8, scale, stats, s); break;
+    case 3: i8_shadow_e4<3>(rows, n, r8, scale, stats, s); break;
+    default: i8_shadow_e4<4>(rows, n, r8, scale, stats, s); break;
+  }
+}
+
+int i8_lists(int num_cus) { return kI8WgPerCu * num_cus; }
+
+template <int E4, int NQ>
+void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
+  const int G = kI8WgPerCu * a.num_cus;
+  const int64_t n_units = (a.n + kI8Rows - 1) / kI8Rows;
+  tl->mark(s, 0);
+  hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_MAX>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8, a.scale,
+                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci);
+  tl->mark(s, 1);
+  hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, G, a.nq, a.tau,
+                     a.count);
+  tl->mark(s, 0);
+  hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_APPEND>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8,
+                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci);
+  tl->mark(s, 1);
+  hipLaunchKernelGGL(bf16_select_kernel, dim3(a.nq), dim3(256), 0, s, a.cs, a.ci, a.count, a.tau, a.kc,
+                     a.out_s, a.out_i);
+}
+
+// one query per launch (the single-query latency path; NQ > 1 costs registers: 256 VGPRs
+// at NQ = 4, dim 768)
+void launch_thresh_i8(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
+  switch (a.dim / 256) {
+    case 1: launch_i8_nq<1, 1>(a, s, tl); break;
+    case 2: launch_i8_nq<2, 1>(a, s, tl); break;
+    case 3: launch_i8_nq<3, 1>(a, s, tl); break;
+    default: launch_i8_nq<4, 1>(a, s, tl); break;
+  }
+}
+
 }  // namespace mq

@@ -30,4 +30,32 @@ struct ThreshArgs {
 // Enqueue the four K9t launches on `s`; timeline stage 0 = the two scans, 1 = tau + select.
 void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl);
 
+// K9q: the int8 threshold scan for one query (single-query certified screen).
+constexpr int kI8WgPerCu = 3;   // 256-thread workgroups per CU (= residency at <= 168 VGPRs: the
+                                // scan loops are persistent, a non-resident 4th would run late)
+constexpr int kI8PadRows = 8;   // the shadow is allocated to whole 8-row units
+struct ThreshI8Args {
+  const float* q;             // fp32 queries [nq][dim]
+  int nq;                     // 1
+  const unsigned* r8;         // int8 shadow [n][dim] (4 elements per dword)
+  const float* scale;         // [n] per-row scales
+  int64_t n;
+  int dim;                    // 256, 512, 768 or 1024
+  int num_cus;
+  int kc;                     // candidates per query (<= MQ_MAX_K)
+  float* lmax;                // [nq][i8_lists(num_cus)] sample-pass workgroup maxima
+  float* tau;                 // [nq]
+  int* count;                 // [nq]
+  float* cs;                  // [nq][kTsCap] survivor scores
+  int* ci;                    // [nq][kTsCap] survivor rows
+  float* out_s;               // [nq][kc] candidates, (score desc, id asc)
+  int64_t* out_i;
+};
+int i8_lists(int num_cus);
+void launch_thresh_i8(const ThreshI8Args& a, hipStream_t s, Timeline* tl);
+// int8 shadow of rows [0, n): r8 [n][dim] int8, scale [n], stats [0] max ||c - scale r8||,
+// [1] max ||scale r8|| (float bits; atomicMax - zero them before the first rows).
+void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, unsigned* stats,
+                      hipStream_t s);
+
 }  // namespace mq

@@ -65,6 +65,7 @@ SIGNATURES = {
     "mq_index_set_precision": (_I, [_P, _I]),
     "mq_index_set_stream_threshold": (_I, [_P, _I]),
     "mq_index_set_threshold_scan": (_I, [_P, _I]),
+    "mq_index_set_int8_screen": (_I, [_P, _I]),
     "mq_index_rescans": (_I, [_P, _P, _P]),
     "mq_index_screen_fallbacks": (_I, [_P, _P, _P]),
     "mq_index_set_timing": (_I, [_P, _I]),
@@ -89,6 +90,7 @@ SIGNATURES = {
     "mq_tokenizer_encode_batch": (_I, [_P, ctypes.POINTER(ctypes.c_char_p), _I, _I, _P, _P,
                                        ctypes.POINTER(_I)]),
     "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mq_debug_int8_screen": (_I, [_P, _P, _I, _P, _P, _P]),
 }
 
 _lib = None

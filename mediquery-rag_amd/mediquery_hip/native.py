@@ -97,6 +97,11 @@ class FlatIndex:
         """Batched bf16 candidate scans: threshold scan (K9t, default) or tiled lists."""
         _lib.call("mq_index_set_threshold_scan", self._h, int(bool(enabled)))
 
+    def set_int8_screen(self, enabled=True):
+        """Single screened queries: int8-shadow threshold scan first (K9q, default) or
+        straight to the bf16 stream tier.  Same results either way."""
+        _lib.call("mq_index_set_int8_screen", self._h, int(bool(enabled)))
+
     @property
     def rescans(self):
         """Searches whose k > 16 list-overflow check fired (re-scanned with 64 lists)."""
