@@ -513,6 +513,117 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
+// K9q finish, one block per query (the single-query int8 screen, fused to save launches
+// on the latency path): the survivors' top-kc by screen score (as bf16_select_kernel:
+// slots past the survivors hold (tau, -1), more than kTsCap survivors -> bound +inf),
+// the exact fp32 re-rank of the prefix that can still reach the top-k (screen >=
+// s_k - 2E, as rerank_kernel), the top-k by (score desc, id asc), and the certificate
+// s_kc + E < e_k (as screen_verify_kernel, mode VERIFY_BF16_Q32 with the int8 maxima).
+__global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict__ Q,
+                                                        const float* __restrict__ rows, int dim,
+                                                        const float* __restrict__ ts_cs,
+                                                        const int* __restrict__ ts_ci,
+                                                        const int* __restrict__ count,
+                                                        const float* __restrict__ tau, int kc, int k,
+                                                        const unsigned* __restrict__ stats,
+                                                        float* __restrict__ os, int64_t* __restrict__ oi,
+                                                        int* __restrict__ n_fail,
+                                                        int64_t* __restrict__ fail) {
+  __shared__ float ls[kTsCap];
+  __shared__ int li[kTsCap];
+  __shared__ float cs[MQ_MAX_K], sc[MQ_MAX_K];
+  __shared__ int ci[MQ_MAX_K];
+  __shared__ long long sid[MQ_MAX_K];
+  __shared__ float e_sh, ek_sh;
+  __shared__ int live_sh;
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int total = count[q];
+  const int cnt = min(total, kTsCap);
+  for (int i = tid; i < cnt; i += 256) {
+    ls[i] = ts_cs[q * kTsCap + i];
+    li[i] = ts_ci[q * kTsCap + i];
+  }
+  if (tid < kc) {
+    cs[tid] = tau[q];
+    ci[tid] = -1;
+    sc[tid] = -INFINITY;
+    sid[tid] = -1;
+  }
+  if (wave == 3) {  // the bound, alongside the survivor loads
+    const float E = screen_bound(Q, dim, q, VERIFY_BF16_Q32, stats, lane);
+    if (lane == 0) {
+      e_sh = E;
+      ek_sh = -INFINITY;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < cnt; i += 256) {
+    const float x = ls[i];
+    const int xi = li[i];
+    int rank = 0;
+    for (int j = 0; j < cnt; ++j) rank += better(ls[j], li[j], x, xi) ? 1 : 0;
+    if (rank < kc) {
+      cs[rank] = rank == kc - 1 && total > kTsCap ? INFINITY : x;
+      ci[rank] = xi;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int live = kc;
+    if (k < kc) {
+      const float cut = cs[k - 1] - 2.f * e_sh;
+      live = max(k, __popcll(__ballot(lane < kc && !(cs[lane] < cut))) + (kc > 64 ? kc - 64 : 0));
+    }
+    if (lane == 0) live_sh = live;
+  }
+  __syncthreads();
+  const int kl = live_sh;
+  const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
+  constexpr int U = MQ_MAX_K / 4;  // every candidate's row load in flight in one round
+  for (int c0 = wave * U; c0 < kl; c0 += 4 * U) {
+    long long id[U];
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      id[u] = c0 + u < kl ? ci[c0 + u] : -1;
+      acc[u] = 0.f;
+    }
+    for (int i = lane; i < dim / 4; i += 64) {
+      const floatx4 a = q4[i];
+      floatx4 b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
+      if (lane == 0 && c0 + u < kl) {
+        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
+        sid[c0 + u] = id[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < kc) {
+    int rank = 0;
+    for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
+    if (rank < k) {
+      const float x = sid[tid] >= 0 ? sc[tid] : -INFINITY;
+      os[q * k + rank] = x;
+      oi[q * k + rank] = sid[tid];
+      if (rank == k - 1) ek_sh = x;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && !(cs[kc - 1] + e_sh < ek_sh)) fail[atomicAdd(n_fail, 1)] = q;
+}
+
 // ======================================================= K10: merge lists ======
 // One block per query.  Each list is sorted, so a thread walks its share of the lists
 // (lists tid, tid+256, ...) reading heads in batches of 8 independent loads, and only
@@ -1191,7 +1302,10 @@ bool i8_ok(mq_index* ix, int64_t nq) {
   return true;
 }
 
-int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t* oi, hipStream_t s) {
+// K9q scans for nq = 1 query, then (os != null) the select of the top-kc candidates;
+// `zero` (optional) is set to 0 by the sample pass.  The timeline stays open (stage 1).
+int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t* oi, hipStream_t s,
+            int* zero = nullptr) {
   const size_t n_lists = (size_t)i8_lists(ix->num_cus);
   int rc = ensure_i8(ix, s);
   if (!rc) rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
@@ -1201,11 +1315,13 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   if (!rc) rc = ix->ts_ci.ensure((size_t)nq * kTsCap * sizeof(int));
   if (rc) return rc;
   ThreshI8Args a{q, (int)nq, ix->rows8.as<unsigned>(), ix->scale8.as<float>(), ix->n, ix->dim, ix->num_cus,
-                 kc, ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
-                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi};
+                 ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
+                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), zero};
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh_i8(a, s, &ix->tl);
-  ix->tl.close(s);
+  ix->tl.mark(s, 1);
+  if (os) launch_select(ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
+                        (int)nq, kc, os, oi, s);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1285,26 +1401,36 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
   if (!rc) rc = ix->flag.ensure(sizeof(int));
   if (!rc) rc = ix->tier_fail[tier].ensure((size_t)nq * sizeof(int64_t));
   if (rc) return rc;
-  const int kind = tier == TIER_X6 ? SCAN_X6 : tier == TIER_BF16 ? SCAN_BF16 : SCAN_STREAM16;
-  const float* qs = tier == TIER_BF16 ? ix->q16.as<float>() : q;
-  rc = tier == TIER_I8 ? i8_topk(ix, q, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
-       : kind == SCAN_BF16
-           ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
-           : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
-  if (rc) return rc;
-  // the int8 screen's bound has the Q32 form (fp32 query) with the int8 shadow's maxima
-  const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
-  const unsigned* stats = bf ? ix->stats16.as<unsigned>() : tier == TIER_I8 ? ix->stats8.as<unsigned>() : nullptr;
-  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
-                     ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), mode, stats);
-  MQ_HIP(hipGetLastError());
-  if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
   int64_t* fail = ix->tier_fail[tier].as<int64_t>();
-  MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
-                     ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
-                     fail);
-  MQ_HIP(hipGetLastError());
+  if (tier == TIER_I8) {
+    // scans (the sample pass zeroes the failure count), then select + re-rank + certificate
+    // in one launch; the int8 screen's bound has the Q32 form (fp32 query) with the int8
+    // shadow's maxima (kc = 64 < n: the int8 tier needs >= kTsMinRows rows)
+    rc = i8_topk(ix, q, nq, kc, nullptr, nullptr, s, ix->flag.as<int>());
+    if (rc) return rc;
+    hipLaunchKernelGGL(i8_finish_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+                       ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
+                       kc, k, ix->stats8.as<unsigned>(), os, oi, ix->flag.as<int>(), fail);
+    ix->tl.close(s);
+    MQ_HIP(hipGetLastError());
+  } else {
+    const int kind = tier == TIER_X6 ? SCAN_X6 : tier == TIER_BF16 ? SCAN_BF16 : SCAN_STREAM16;
+    const float* qs = tier == TIER_BF16 ? ix->q16.as<float>() : q;
+    rc = kind == SCAN_BF16 ? bf16_candidates(ix, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s)
+                           : scan_topk(ix, kind, qs, nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s);
+    if (rc) return rc;
+    const int mode = tier == TIER_X6 ? VERIFY_X6 : tier == TIER_BF16 ? VERIFY_BF16_Q16 : VERIFY_BF16_Q32;
+    const unsigned* stats = bf ? ix->stats16.as<unsigned>() : nullptr;
+    hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+                       ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), mode, stats);
+    MQ_HIP(hipGetLastError());
+    if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
+    MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
+                       ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
+                       fail);
+    MQ_HIP(hipGetLastError());
+  }
   int n_fail = 0;
   MQ_HIP(hipMemcpyAsync(&n_fail, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
@@ -1605,6 +1731,7 @@ int mq_debug_int8_screen(mq_index* ix, const float* query, int kc, float* out_sc
   if (rc) return rc;
   MQ_HIP(hipMemcpyAsync(ix->stage.p, query, (size_t)ix->dim * 4, hipMemcpyHostToDevice, s));
   rc = i8_topk(ix, ix->stage.as<float>(), 1, kc, ix->out_s.as<float>(), ix->out_i.as<int64_t>(), s);
+  ix->tl.close(s);
   if (rc) return rc;
   MQ_HIP(hipMemcpyAsync(out_scores, ix->out_s.p, (size_t)kc * 4, hipMemcpyDeviceToHost, s));
   MQ_HIP(hipMemcpyAsync(out_ids, ix->out_i.p, (size_t)kc * 8, hipMemcpyDeviceToHost, s));

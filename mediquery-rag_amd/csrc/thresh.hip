@@ -342,7 +342,8 @@ void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
 // screen score of row c is fl(scale_c * fl(sum_j q_j r8_cj)) with the fp32 query; its
 // error against the exact dot is bounded as in VERIFY_BF16_Q32 with the int8 shadow's own
 // maxima (dmax = max ||c - scale_c r8_c||, cmax = max ||scale_c r8_c||).  Same threshold
-// scheme as K9t (sample pass -> tau -> appending pass -> select), on the VALU: lane l
+// scheme as K9t (sample pass -> tau -> appending pass -> select; tau is found inside the
+// appending pass, the select fused with the re-rank in index.hip), on the VALU: lane l
 // holds elements [l E, l E + E) of every row (E = dim / 64) and of the query, in
 // registers; a wave takes 8 rows per step (8 x dim bytes, contiguous), converts and
 // multiplies, and one transposed butterfly (xor 32 / 16 / 8 halving the values, then
@@ -396,7 +397,18 @@ __global__ __launch_bounds__(256) void i8_shadow_kernel(const float* __restrict_
   }
 }
 
-constexpr int kI8Rows = 8;  // rows per wave step
+// order-preserving float <-> unsigned (key 0 is below every float)
+__device__ __forceinline__ unsigned ord_key(float x) {
+  const unsigned b = __float_as_uint(x);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float key_ord(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+constexpr int kI8Rows = 8;    // rows per wave step
+constexpr int kI8Stages = 2;  // register stages of the row stream (1 step in flight; a
+                              // third spills at dim 768 under the 3-workgroup budget)
 
 // values v[0 .. 8 NQ) indexed r * NQ + q -> lane l holds v[0 .. NQ) of row
 // 4 b5(l) + 2 b4(l) + b3(l), summed over the 64 lanes
@@ -418,15 +430,17 @@ __device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int l
     for (int i = 0; i < NQ; ++i) v[i] += __shfl_xor(v[i], m);
 }
 
+// One 8-row unit: rows past n_rows read the shadow's padding (allocated to whole units;
+// their scores are never used), so the unit is one base address + immediate offsets.
 template <int E4>
-__device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t n_rows, int64_t unit,
-                                        int lane, unsigned (&a)[kI8Rows][E4]) {
+__device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t unit, int lane,
+                                        unsigned (&a)[kI8Rows][E4]) {
   constexpr int DIM4 = 64 * E4;  // dwords per row (dim = 256 E4 one-byte elements)
 #pragma unroll
   for (int r = 0; r < kI8Rows; ++r) {
-    const int64_t row = min(unit * kI8Rows + r, n_rows - 1);
+    const unsigned* p = r8 + (unit * kI8Rows + r) * DIM4 + lane * E4;
 #pragma unroll
-    for (int d = 0; d < E4; ++d) a[r][d] = r8[row * DIM4 + lane * E4 + d];
+    for (int d = 0; d < E4; ++d) a[r][d] = p[d];
   }
 }
 
@@ -453,9 +467,10 @@ __device__ __forceinline__ void i8_dot(const unsigned (&a)[kI8Rows][E4], const f
 template <int E4, int NQ, int MODE>
 __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
     const float* __restrict__ Q, int nq, const unsigned* __restrict__ r8, const float* __restrict__ scale,
-    int64_t n_rows, int64_t n_units, int period, const float* __restrict__ tau, float* __restrict__ lmax,
-    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci) {
+    int64_t n_rows, int64_t n_units, int period, float* __restrict__ tau, const float* __restrict__ lmax_in,
+    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci, int* __restrict__ zero) {
   constexpr int E = 4 * E4, DIM = 64 * E;
+  float* lmax = const_cast<float*>(lmax_in);  // written by TS_MAX, read by TS_APPEND
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int W = gridDim.x * 4;
@@ -475,18 +490,20 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
   float th[NQ], mx[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    th[q] = MODE == TS_APPEND ? tau[min(q, nq - 1)] : 0.f;
+    th[q] = 0.f;
     mx[q] = -INFINITY;
   }
+  if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x < NQ) count[threadIdx.x] = 0;
+  if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x == 0 && zero) *zero = 0;  // caller's flag
   const int my_r = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
   const int64_t stride = (int64_t)W * period;
-  unsigned a[2][kI8Rows][E4];
-  float sc[2];
+  unsigned a[kI8Stages][kI8Rows][E4];
+  float sc[kI8Stages];
   int64_t u = (int64_t)gw * period;
   auto fetch = [&](int buf, int64_t unit) {
     const int64_t uu = min(unit, n_units - 1);  // past the end: re-read the last unit
-    i8_load<E4>(r8, n_rows, uu, lane, a[buf]);
-    sc[buf] = scale[min(uu * kI8Rows + my_r, n_rows - 1)];
+    i8_load<E4>(r8, uu, lane, a[buf]);
+    sc[buf] = scale[uu * kI8Rows + my_r];  // (padding rows: allocated, unused)
   };
   auto consume = [&](int buf, int64_t unit) {
     float v[kI8Rows * NQ];
@@ -508,7 +525,50 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       }
     }
   };
+  // kI8Stages register stages: the next kI8Stages - 1 units' loads are in flight while
+  // one is multiplied (stage indices are compile-time: no register indexing)
+  // tau per query from the sample pass's n_lists = gridDim.x workgroup maxima, computed
+  // in every workgroup by wave 0 (same inputs, same steps: the same tau everywhere)
+  // instead of a separate launch: the kTsRank-th largest maximum by a bitwise search on
+  // order-preserving keys with ballot counts; workgroup 0 stores it for the select.  The
+  // maxima are loaded before the first rows, so the search runs under their latency.
+  constexpr int kPer = kI8MaxLists / 64;  // lists per lane
+  __shared__ float th_sh[NQ];
+  const bool tau_wave = MODE == TS_APPEND && (threadIdx.x >> 6) == 0;
+  unsigned key[NQ][kPer];
+  if (tau_wave) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int l = lane + 64 * j;
+        key[q][j] = l < (int)gridDim.x ? ord_key(lmax[(int64_t)min(q, nq - 1) * gridDim.x + l]) : 0u;
+      }
+  }
   if (u < n_units) fetch(0, u);
+  if (MODE == TS_APPEND) {
+    if (tau_wave) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        unsigned T = 0;
+        for (int b = 31; b >= 0; --b) {
+          const unsigned cand = T | (1u << b);
+          int c = 0;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) c += __popcll(__ballot(key[q][j] >= cand));
+          if (c >= kTsRank) T = cand;
+        }
+        const float t = T == 0u ? -INFINITY : key_ord(T);
+        if (lane == 0) {
+          th_sh[q] = t;
+          if (blockIdx.x == 0 && q < nq) tau[q] = t;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) th[q] = th_sh[q];
+  }
   // two register stages: the next unit's loads are in flight while one is multiplied
   while (u < n_units) {
     const int64_t u1 = u + stride;
@@ -554,24 +614,22 @@ void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float
   }
 }
 
-int i8_lists(int num_cus) { return kI8WgPerCu * num_cus; }
+int i8_lists(int num_cus) { return std::min(kI8WgPerCu * num_cus, kI8MaxLists); }
 
 template <int E4, int NQ>
 void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
-  const int G = kI8WgPerCu * a.num_cus;
+  const int G = i8_lists(a.num_cus);
   const int64_t n_units = (a.n + kI8Rows - 1) / kI8Rows;
   tl->mark(s, 0);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_MAX>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8, a.scale,
-                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci);
-  tl->mark(s, 1);
-  hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, G, a.nq, a.tau,
-                     a.count);
-  tl->mark(s, 0);
+                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_APPEND>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8,
-                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci);
-  tl->mark(s, 1);
-  hipLaunchKernelGGL(bf16_select_kernel, dim3(a.nq), dim3(256), 0, s, a.cs, a.ci, a.count, a.tau, a.kc,
-                     a.out_s, a.out_i);
+                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr);
+}
+
+void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,
+                   float* out_s, int64_t* out_i, hipStream_t s) {
+  hipLaunchKernelGGL(bf16_select_kernel, dim3(nq), dim3(256), 0, s, cs, ci, count, tau, kc, out_s, out_i);
 }
 
 // one query per launch (the single-query latency path; NQ > 1 costs registers: 256 VGPRs

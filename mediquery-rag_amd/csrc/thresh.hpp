@@ -33,6 +33,7 @@ void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl);
 // K9q: the int8 threshold scan for one query (single-query certified screen).
 constexpr int kI8WgPerCu = 3;   // 256-thread workgroups per CU (= residency at <= 168 VGPRs: the
                                 // scan loops are persistent, a non-resident 4th would run late)
+constexpr int kI8MaxLists = 1024;  // workgroups per launch = sample lists (tau is found in-kernel)
 constexpr int kI8PadRows = 8;   // the shadow is allocated to whole 8-row units
 struct ThreshI8Args {
   const float* q;             // fp32 queries [nq][dim]
@@ -42,17 +43,19 @@ struct ThreshI8Args {
   int64_t n;
   int dim;                    // 256, 512, 768 or 1024
   int num_cus;
-  int kc;                     // candidates per query (<= MQ_MAX_K)
   float* lmax;                // [nq][i8_lists(num_cus)] sample-pass workgroup maxima
   float* tau;                 // [nq]
   int* count;                 // [nq]
   float* cs;                  // [nq][kTsCap] survivor scores
   int* ci;                    // [nq][kTsCap] survivor rows
-  float* out_s;               // [nq][kc] candidates, (score desc, id asc)
-  int64_t* out_i;
+  int* zero;                  // optional int the sample pass sets to 0 (the caller's fail count)
 };
 int i8_lists(int num_cus);
+// The sample and appending passes: survivors in cs / ci / count, tau in tau.
 void launch_thresh_i8(const ThreshI8Args& a, hipStream_t s, Timeline* tl);
+// Survivors -> top-kc candidates per query (K9t's select; slots past the count: (tau, -1)).
+void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,
+                   float* out_s, int64_t* out_i, hipStream_t s);
 // int8 shadow of rows [0, n): r8 [n][dim] int8, scale [n], stats [0] max ||c - scale r8||,
 // [1] max ||scale r8|| (float bits; atomicMax - zero them before the first rows).
 void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, unsigned* stats,
