@@ -264,10 +264,19 @@ def main():
                "ms_per_step": round(t2 * 1e3, 3),
                "encoder_tflops_effective": round(encoder_flops(cfg, B, L2) / t2 / 1e12, 2)}
 
+    traffic_db_early = {}
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic_db_early = json.load(open(pmc))
+        except Exception:
+            traffic_db_early = {}
+
     # ---- single-query latency (embed 1 query + search the shard), exact f32 ----------
-    lat = []
+    lat, lat_parts, single_roof = [], None, None
     if world == 1 and args.single_iters > 0:
         ids1, mask1, q1 = ids[:1].contiguous(), mask[:1].contiguous(), q[:1]
+        pd0 = index.screen_passdowns
         for it in range(args.single_iters + 5):
             torch.cuda.synchronize()
             a = time.perf_counter()
@@ -276,6 +285,35 @@ def main():
             torch.cuda.synchronize()
             if it >= 5:
                 lat.append((time.perf_counter() - a) * 1e3)
+        enc_l, srch_l = [], []  # the two halves alone (a host sync between them)
+        for it in range(args.single_iters):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            enc.embed_device(ids1, mask1, q1)
+            torch.cuda.synchronize()
+            b = time.perf_counter()
+            local_search(q1, K)
+            torch.cuda.synchronize()
+            enc_l.append((b - a) * 1e3)
+            srch_l.append((time.perf_counter() - b) * 1e3)
+        lat_parts = {"encoder_ms": round(statistics.median(enc_l), 3),
+                     "search_ms": round(statistics.median(srch_l), 3),
+                     "search_tier": "int8 screen (K9q) -> fp32 re-rank + certificate",
+                     "passdowns": index.screen_passdowns - pd0}
+        # the single query's scan: K9q sample + appending pass over the int8 shadow (HBM-bound)
+        index.read_timing()
+        index.set_timing(True)
+        for _ in range(20):
+            local_search(q1, K)
+        scan_ms = index.read_timing()["flat_search_kernel"] / 20
+        index.set_timing(False)
+        i8_bytes = cnt * (768 + 4) * (1 + 1 / 16)  # appending pass + 1/16 sample pass
+        single_roof = {"kernel": "i8_thresh_kernel (K9q: sample + appending pass)", "bound": "hbm",
+                       "achieved": round(i8_bytes / (scan_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(i8_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "bytes_per_search": int(i8_bytes), "ms_per_search": round(scan_ms, 4),
+                       "traffic": (traffic_db_early.get("i8_thresh_kernel", 0) + traffic_db_early.get("i8_thresh_sample", 0))
+                       or None}
 
     if rank != 0:
         if world > 1:
@@ -295,13 +333,7 @@ def main():
         "ffn_down_gemm": (full_l * M + last * B) * 2.0 * H * F,
         "flat_search_kernel": 2.0 * nq_all * cnt * 768,
     }
-    traffic_db = {}
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            traffic_db = json.load(open(pmc))
-        except Exception:
-            traffic_db = {}
+    traffic_db = traffic_db_early
     srch_bytes = cnt * 768 * 4 + nq_all * 768 * 4 + nq_all * K * 12
 
     X6_PEAK = BF16_PEAK_TFLOPS / 6.0  # six bf16 MFMAs per fp32 product: 417 TFLOP/s fp32-equiv.
@@ -371,6 +403,8 @@ def main():
                    "encoder": "BERT-base %dL (dmeta-embedding-zh shape)" % cfg.layers,
                    "parallelism": "row-shard x%d + DP encoder" % world if world > 1 else "single GPU"},
         "p50_single_query_ms": round(statistics.median(lat), 3) if lat else None,
+        "p50_single_query_parts": lat_parts,
+        "single_query_search_roofline": single_roof,
         "planted_top1_ok": main_r["planted_top1_ok"],
         "roofline": main_r["roofline"],
         "search_roofline": main_r["search_roofline"],

@@ -66,6 +66,8 @@ CLASSES = {
     "flat_search_kernel_bf16": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, true>, 8>",
     "bf16_thresh_kernel": r"bf16_thresh_kernel<\d+, 1>",
     "bf16_thresh_sample": r"bf16_thresh_kernel<\d+, 0>",
+    "i8_thresh_kernel": r"i8_thresh_kernel<\d, 1, 1>",
+    "i8_thresh_sample": r"i8_thresh_kernel<\d, 1, 0>",
     "qkv_gemm": r"gemm_nt_kernel<mq::F32Tile<\d, \d, \d, \d, false, \d, false>, 0>",
     "ffn_up_gemm": r"gemm_nt_kernel<mq::F32Tile<\d, \d, \d, \d, false, \d, false>, [12]>",
     "out_proj_gemm": r"gemm_nt_kernel<mq::F32Tile<\d, \d, \d, \d, false, \d, false>, 3>",
