@@ -178,9 +178,11 @@ int mq_encoder_set_precision(mq_encoder* enc, int dtype);
  * [0] embed+LN, [1] QKV GEMM, [2] attention, [3] out-proj GEMM, [4] LayerNorm,
  * [5] FFN-up GEMM, [6] FFN-down GEMM, [7] pool+normalise, and resets them. */
 #define MQ_ENC_STAGES 8
-/* Replay each forward shape as a captured hipGraph (default on; off while timing is
- * on).  Results are bit-identical either way; graphs cut per-kernel launch cost, which
- * dominates small batches (single-query latency). */
+/* Replay each forward shape as a captured hipGraph (default off; never while timing is
+ * on).  Results are bit-identical either way.  On MI355X the host enqueues the ~110
+ * launches of a forward faster than the device runs them, so eager launches measured
+ * faster for one query (0.628 vs 0.645 ms: the graph path stages ids / mask / out through
+ * its own captured buffers); graphs help a host-bound caller. */
 int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);
 int mq_encoder_read_timing(mq_encoder* enc, float* ms, int n);

@@ -207,7 +207,8 @@ class Encoder:
         _lib.call("mq_encoder_set_precision", self._h, dtype)
 
     def set_graphs(self, enabled=True):
-        """Replay forwards as captured hipGraphs (default on; bit-identical results)."""
+        """Replay forwards as captured hipGraphs (default off: eager measured faster on
+        MI355X for one query; bit-identical results)."""
         _lib.call("mq_encoder_set_graphs", self._h, int(bool(enabled)))
 
     def embed(self, ids, mask):
