@@ -406,16 +406,29 @@ __device__ __forceinline__ float key_ord(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-constexpr int kI8Rows = 8;    // rows per wave step
+#ifndef MQ_I8_ROWS
+#define MQ_I8_ROWS 8
+#endif
+constexpr int kI8Rows = MQ_I8_ROWS;  // rows per wave step (8 or 16)
 constexpr int kI8Stages = 2;  // register stages of the row stream (1 step in flight; a
                               // third spills at dim 768 under the 3-workgroup budget)
+constexpr int kI8Lg = kI8Rows == 16 ? 4 : 3;
+static_assert(kI8Rows == 1 << kI8Lg, "8 or 16 rows per step");
 
-// values v[0 .. 8 NQ) indexed r * NQ + q -> lane l holds v[0 .. NQ) of row
-// 4 b5(l) + 2 b4(l) + b3(l), summed over the 64 lanes
+// values v[0 .. R NQ) indexed r * NQ + q -> lane l holds v[0 .. NQ) of row i8_row(l),
+// summed over the 64 lanes: log2 R halving exchanges (xor 32, 16, ...), then a plain
+// butterfly over the remaining lane bits
+__device__ __forceinline__ int i8_row(int lane) {
+  int r = 0;
+#pragma unroll
+  for (int i = 0; i < kI8Lg; ++i) r |= ((lane >> (5 - i)) & 1) << (kI8Lg - 1 - i);
+  return r;
+}
+
 template <int NQ>
 __device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int lane) {
 #pragma unroll
-  for (int m = 32, c = kI8Rows * NQ; m >= 8; m >>= 1, c >>= 1) {
+  for (int m = 32, c = kI8Rows * NQ; m >= 64 / kI8Rows; m >>= 1, c >>= 1) {
     const bool hi = (lane & m) != 0;
 #pragma unroll
     for (int i = 0; i < c / 2; ++i) {
@@ -425,13 +438,11 @@ __device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int l
     }
   }
 #pragma unroll
-  for (int m = 4; m > 0; m >>= 1)
+  for (int m = 32 / kI8Rows; m > 0; m >>= 1)
 #pragma unroll
     for (int i = 0; i < NQ; ++i) v[i] += __shfl_xor(v[i], m);
 }
 
-// One 8-row unit: rows past n_rows read the shadow's padding (allocated to whole units;
-// their scores are never used), so the unit is one base address + immediate offsets.
 template <int E4>
 __device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t unit, int lane,
                                         unsigned (&a)[kI8Rows][E4]) {
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
   }
   if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x < NQ) count[threadIdx.x] = 0;
   if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x == 0 && zero) *zero = 0;  // caller's flag
-  const int my_r = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+  const int my_r = i8_row(lane);
   const int64_t stride = (int64_t)W * period;
   unsigned a[kI8Stages][kI8Rows][E4];
   float sc[kI8Stages];
@@ -516,7 +527,7 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       const float score = v[q] * sc[buf];
       if (MODE == TS_MAX) {
         mx[q] = valid ? fmaxf(mx[q], score) : mx[q];
-      } else if ((lane & 7) == 0 && valid && q < nq && score >= th[q]) {
+      } else if ((lane & (64 / kI8Rows - 1)) == 0 && valid && q < nq && score >= th[q]) {
         const int slot = atomicAdd(count + q, 1);
         if (slot < kTsCap) {
           cs[(int64_t)q * kTsCap + slot] = score;

@@ -31,10 +31,13 @@ struct ThreshArgs {
 void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl);
 
 // K9q: the int8 threshold scan for one query (single-query certified screen).
-constexpr int kI8WgPerCu = 3;   // 256-thread workgroups per CU (= residency at <= 168 VGPRs: the
+#ifndef MQ_I8_WG
+#define MQ_I8_WG 3
+#endif
+constexpr int kI8WgPerCu = MQ_I8_WG;   // 256-thread workgroups per CU (= residency at <= 168 VGPRs: the
                                 // scan loops are persistent, a non-resident 4th would run late)
 constexpr int kI8MaxLists = 1024;  // workgroups per launch = sample lists (tau is found in-kernel)
-constexpr int kI8PadRows = 8;   // the shadow is allocated to whole 8-row units
+constexpr int kI8PadRows = 16;  // the shadow is allocated to whole 8- or 16-row units
 struct ThreshI8Args {
   const float* q;             // fp32 queries [nq][dim]
   int nq;                     // 1
