@@ -309,6 +309,149 @@ __global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(
   }
 }
 
+// Row statistics of one LayerNorm row held as ln_row_store holds it (same sums in the
+// same order, so mean / rstd are bitwise those of ln_kernel).
+template <int VPL>
+__device__ __forceinline__ void ln_row_stats(const floatx4 (&x)[VPL], float eps, float& mean,
+                                             float& rstd) {
+  constexpr int H = VPL * 256;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += x[i].x + x[i].y + x[i].z + x[i].w;
+  mean = wave_sum(s) * (1.0f / H);
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const floatx4 d = x[i] - mean;
+    v += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+  }
+  rstd = 1.0f / sqrtf(wave_sum(v) * (1.0f / H) + eps);
+}
+
+// ------------------------------------------------------- few-row GEMM (K2r) ----
+// A single query is M = L <= 64 token rows: the tiled GEMM leaves the chip idle and the
+// split-K path pays a second launch for its ordered slab reduction (~5 us each, 4 per
+// layer).  Here one 1024-thread workgroup owns a 16 x 16 output tile over the FULL depth:
+// its 16 waves each multiply one contiguous K range (NB x 256 / 16 deep) on
+// v_mfma_f32_16x16x4_f32 and the 16 partial tiles are summed in wave order through LDS
+// (bitwise reproducible), then bias / GELU / residual.  Grid (N / 16, ceil(M / 16)):
+// 288 workgroups for QKV, 384 for FFN-up, 96 for the two H-wide projections at M = 32.
+// Lane (c = l & 15, kq = l >> 4) loads float4s of row c of the A and W tiles at
+// k0 + 4 kq; MFMA step t multiplies element t, i.e. logical k index kq <-> k0 + 4 kq + t
+// in both operands.
+// LN_IN: A holds pre-LayerNorm rows (the last residual sum, K = H = 256 VPL); wave w
+// first computes row r0 + w's mean / rstd (as ln_kernel) and A is normalised while it is
+// loaded, so no LayerNorm launch sits between the GEMMs.  The column-0 workgroups also
+// store the normalised rows to ln_out: the residual input of the next projection.
+constexpr int kRT = 16;      // rows = columns per output tile
+constexpr int kRWaves = 16;  // waves per workgroup, one K range each
+constexpr int kRowsMax = 64; // token rows up to which a forward takes this path
+
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
+__global__ __launch_bounds__(1024) void rows_gemm_kernel(
+    const float* __restrict__ A, int lda, int64_t a_plane, int M, const float* __restrict__ lng,
+    const float* __restrict__ lnb, float eps, float* __restrict__ ln_out,
+    const float* __restrict__ W, int ldw, const float* __restrict__ bias,
+    const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane) {
+  constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
+  // 16-deep blocks per load batch: all of them up to 12 (96 VGPRs of operands in flight,
+  // one memory round trip), else batches of 8
+  constexpr int CH = NB <= 12 ? NB : 8;
+  static_assert(NB % CH == 0, "NB must be <= 12 or a multiple of 8");
+  static_assert(!LN_IN || NB == VPL, "LayerNorm input needs K == H");
+  // LN_IN: the 16 normalised rows, row stride K + 4 floats (a 16-lane ds_read_b128 group
+  // reads 16 rows at one k: 16 distinct 16-B bank groups)
+  constexpr int AS = K + 4;
+  __shared__ __attribute__((aligned(16))) float arows[LN_IN ? kRT * AS : 4];
+  __shared__ float part[kRWaves][kRT * kRT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, kq = lane >> 4;
+  const int n0 = blockIdx.x * kRT, r0 = blockIdx.y * kRT;
+  const int kb0 = wave * (K / kRWaves);  // this wave's K range
+  const int ks = blockIdx.z;  // K split: columns [ks K, (ks + 1) K) of A and W
+  const float* wrow = W + (int64_t)(n0 + c) * ldw + ks * K + kb0 + 4 * kq;
+  const float* arow = A + (int64_t)min(r0 + c, M - 1) * lda + ks * K + kb0 + 4 * kq;
+
+  floatx4 wv[CH], av[CH];
+  // the first batch of weights is in flight before anything else (the LayerNorm pass
+  // below waits on its own row loads only)
+#pragma unroll
+  for (int j = 0; j < CH; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+  if (LN_IN) {
+    const int row = r0 + wave;  // one wave per row (kRWaves == kRT)
+    const float* src = A + (int64_t)min(row, M - 1) * lda;
+    // the row is the sum of S_IN split-K planes of the producing GEMM, added in order
+    floatx4 p[S_IN][VPL];
+#pragma unroll
+    for (int z = 0; z < S_IN; ++z)
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) p[z][i] = *reinterpret_cast<const floatx4*>(src + z * a_plane + (i * 64 + lane) * 4);
+    floatx4 x[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      x[i] = p[0][i];
+#pragma unroll
+      for (int z = 1; z < S_IN; ++z) x[i] += p[z][i];
+    }
+    float mu, rs;
+    ln_row_stats<VPL>(x, eps, mu, rs);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int cc = (i * 64 + lane) * 4;
+      x[i] = (x[i] - mu) * rs * *reinterpret_cast<const floatx4*>(lng + cc) +
+             *reinterpret_cast<const floatx4*>(lnb + cc);
+      *reinterpret_cast<floatx4*>(&arows[wave * AS + cc]) = x[i];
+    }
+    if (ln_out && blockIdx.x == 0 && row < M) {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i)
+        *reinterpret_cast<floatx4*>(ln_out + (int64_t)row * K + (i * 64 + lane) * 4) = x[i];
+    }
+    // LDS-only barrier: the weight loads stay in flight across it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < NB; b += CH) {
+    if (b > 0) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * (b + j));
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (LN_IN)
+        av[j] = *reinterpret_cast<const floatx4*>(&arows[c * AS + kb0 + 16 * (b + j) + 4 * kq]);
+      else
+        av[j] = *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], wv[j][t], acc, 0, 0, 0);
+    }
+  }
+  // accumulator element j is (row 4 kq + j, column c) of this wave's partial tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) part[wave][(4 * kq + j) * kRT + c] = acc[j];
+  __syncthreads();
+  if (threadIdx.x >= kRT * kRT) return;
+  const int rr = threadIdx.x / kRT, cc = threadIdx.x % kRT;
+  const int row = r0 + rr, col = n0 + cc;
+  float v = part[0][threadIdx.x];
+#pragma unroll
+  for (int w = 1; w < kRWaves; ++w) v += part[w][threadIdx.x];
+  if (row >= M) return;
+  if (ks == 0) {  // split 0 carries bias / residual; GELU needs an unsplit K
+    v += bias[col];
+    if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+    if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+    if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+  }
+  out[ks * o_plane + (int64_t)row * ldo + col] = v;
+}
+
 // One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).
 template <int VPL>
 __global__ __launch_bounds__(256) void embed_ln_kernel(
@@ -484,6 +627,64 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ hs,
 #pragma unroll
     for (int i = 0; i < VPL; ++i)
       x[i] = *reinterpret_cast<const floatx4*>(hs + (int64_t)b * L * H + (i * 64 + lane) * 4);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) ss += x[i].x * x[i].x + x[i].y * x[i].y + x[i].z * x[i].z + x[i].w * x[i].w;
+  const float inv = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+    *reinterpret_cast<floatx4*>(out + (int64_t)b * H + (i * 64 + lane) * 4) = x[i] * inv;
+}
+
+// K7 for the few-row path, whose last layer leaves pre-LayerNorm rows as `planes`
+// split-K planes (`plane` floats apart, summed in order): LN (g, be) of the pooled rows,
+// then pool and L2-normalise as pool_kernel.  `rows` = rows per sequence in hs (1: the
+// compact CLS rows of the pruned last layer).
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_pool_kernel(const float* __restrict__ hs, int planes,
+                                                      int64_t plane, const int* __restrict__ mask,
+                                                      int B, int L, int rows, int pooling,
+                                                      const float* __restrict__ g,
+                                                      const float* __restrict__ be, float eps,
+                                                      float* __restrict__ out) {
+  constexpr int H = VPL * 256;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  auto ln_row = [&](const float* src, floatx4 (&x)[VPL]) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) x[i] = *reinterpret_cast<const floatx4*>(src + (i * 64 + lane) * 4);
+    for (int z = 1; z < planes; ++z)
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) x[i] += *reinterpret_cast<const floatx4*>(src + z * plane + (i * 64 + lane) * 4);
+    float mu, rs;
+    ln_row_stats<VPL>(x, eps, mu, rs);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      x[i] = (x[i] - mu) * rs * *reinterpret_cast<const floatx4*>(g + c) +
+             *reinterpret_cast<const floatx4*>(be + c);
+    }
+  };
+  floatx4 x[VPL];
+  if (pooling == MQ_POOL_MEAN) {
+    float cnt = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) x[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < L; ++r) {
+      if (!mask[(int64_t)b * L + r]) continue;
+      cnt += 1.f;
+      floatx4 y[VPL];
+      ln_row(hs + ((int64_t)b * rows + r) * H, y);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) x[i] += y[i];
+    }
+    const float inv = 1.0f / fmaxf(cnt, 1.f);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) x[i] *= inv;
+  } else {
+    ln_row(hs + (int64_t)b * rows * H, x);
   }
   float ss = 0.f;
 #pragma unroll
@@ -795,17 +996,167 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
   return MQ_OK;
 }
 
+// ------------------------------------------------------- few-row forward ------
+struct RowsArgs {
+  const float* A;
+  int lda;
+  int64_t a_plane;  // LN_IN: floats between the summed input planes
+  const float* W;
+  int ldw;
+  const float* bias;
+  const float* resid;
+  int ldr;
+  float* out;
+  int ldo;
+  int64_t o_plane;  // floats between the output planes of a K split
+  int M, N, K;      // K: full depth (ldw >= K)
+  int splits;       // K splits (grid.z), each writing one output plane
+};
+
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
+void launch_rows_nb(const RowsArgs& g, const float* lng, const float* lnb, float eps, float* ln_out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN>),
+                     dim3(g.N / kRT, (g.M + kRT - 1) / kRT, g.splits), dim3(64 * kRWaves), 0, s, g.A,
+                     g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
+                     g.out, g.ldo, g.o_plane);
+}
+
+// Per-split depths the few-row kernel is instantiated for (K / 256 blocks per wave).
+bool rows_nb_ok(int nb) { return nb >= 1 && (nb <= 4 || nb == 8 || nb == 12 || nb == 16); }
+
+// K splits for a depth-K projection: per-split depth <= 1024 (more workgroups pull the
+// weights: at K = 3072 one split is 13.9 us, three 128 KB splits are cheaper even with
+// the planes summed by the consumer), at most 4.
+int rows_splits(int K) {
+  const int nb = K / 256;
+  if (nb > 4 && nb % 4 == 0 && nb / 4 <= 4) return nb / 4;
+  return 1;
+}
+
+template <int EPI, int NB>
+void launch_rows_plain(const RowsArgs& g, hipStream_t s) {
+  launch_rows_nb<EPI, false, 1, NB, 1>(g, nullptr, nullptr, 0.f, nullptr, s);
+}
+
+// No LayerNorm on A: any instantiated per-split depth.
+template <int EPI>
+void launch_rows(const RowsArgs& g, hipStream_t s) {
+  switch (g.K / g.splits / 256) {
+    case 1: launch_rows_plain<EPI, 1>(g, s); return;
+    case 2: launch_rows_plain<EPI, 2>(g, s); return;
+    case 3: launch_rows_plain<EPI, 3>(g, s); return;
+    case 4: launch_rows_plain<EPI, 4>(g, s); return;
+    case 8: launch_rows_plain<EPI, 8>(g, s); return;
+    case 12: launch_rows_plain<EPI, 12>(g, s); return;
+    default: launch_rows_plain<EPI, 16>(g, s); return;
+  }
+}
+
+// A = LN(sum of s_in planes) with K == H, the normalised rows also to ln_out (may be null).
+template <int EPI, int VPL>
+void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* lnb, float eps,
+                    float* ln_out, hipStream_t s) {
+  switch (s_in) {
+    case 1: launch_rows_nb<EPI, true, VPL, VPL, 1>(g, lng, lnb, eps, ln_out, s); return;
+    case 2: launch_rows_nb<EPI, true, VPL, VPL, 2>(g, lng, lnb, eps, ln_out, s); return;
+    case 3: launch_rows_nb<EPI, true, VPL, VPL, 3>(g, lng, lnb, eps, ln_out, s); return;
+    default: launch_rows_nb<EPI, true, VPL, VPL, 4>(g, lng, lnb, eps, ln_out, s); return;
+  }
+}
+
+// Few-row forward (B * L <= kRowsMax): 5 launches per layer instead of 9.  Between
+// layers the activations stay pre-LayerNorm, as the FFN-down's split-K planes in `slab`;
+// the next GEMM sums and normalises them on load (K2r LN_IN) and materialises the
+// normalised rows in x for the residual:
+//   QKV   qkv = LN2'(sum slab) Wqkv^T + b  (x = LN2'(...); layer 0 reads the embedding LN x)
+//   attn  ctx
+//   oproj y = ctx Wo^T + bo + x
+//   up    ffn = GELU(LN1(y) W1^T + b1)     (x = LN1(y))
+//   down  slab[z] = ffn[:, Kz] W2[:, Kz]^T (+ b2 + x for z = 0)
+// and ln_pool applies the last LN2 to the pooled rows.  The CLS-only last layer carries
+// the B CLS rows past attention as forward_vpl does.
+template <int VPL>
+int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, float* out,
+                 hipStream_t s) {
+  const mq_bert_config& c = e->cfg;
+  const int M = B * L, H = c.hidden, F = c.ffn;
+  const float eps = c.ln_eps;
+  const float scale = 1.0f / sqrtf((float)(H / c.heads));
+  const int q_tiles = (L + 31) / 32;
+  const int dsplit = rows_splits(F);
+  e->tl.mark(s, ST_EMBED);
+  hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, ids, M, L,
+                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, eps, e->x.p);
+  int prev_rows = M;
+  for (size_t li = 0; li < e->layers.size(); ++li) {
+    const LayerW& w = e->layers[li];
+    const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
+    const int rows = cls_only ? B : M;
+    const int stride = cls_only ? L * H : H;
+    e->tl.mark(s, ST_QKV);
+    if (li == 0) {
+      launch_rows<EPI_BIAS>({e->x.p, H, 0, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1}, s);
+    } else {
+      const LayerW& p = e->layers[li - 1];
+      launch_rows_ln<EPI_BIAS, VPL>({e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p,
+                                     3 * H, 0, M, 3 * H, H, 1},
+                                    dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
+    }
+    e->tl.mark(s, ST_ATTN);
+    const int qt = cls_only ? 1 : q_tiles;
+    hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
+                       H, c.heads, qt, scale, e->ctx.p);
+    e->tl.mark(s, ST_OPROJ);
+    launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
+    e->tl.mark(s, ST_FFN_UP);
+    const RowsArgs up{e->y.p, H, 0, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
+    if (c.gelu == MQ_GELU_TANH)
+      launch_rows_ln<EPI_GELU_TANH, VPL>(up, 1, w.ln1g, w.ln1b, eps, e->x.p, s);
+    else
+      launch_rows_ln<EPI_GELU_ERF, VPL>(up, 1, w.ln1g, w.ln1b, eps, e->x.p, s);
+    e->tl.mark(s, ST_FFN_DOWN);
+    launch_rows<EPI_RESID>({e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F,
+                            dsplit},
+                           s);
+    prev_rows = rows;
+  }
+  e->tl.mark(s, ST_POOL);
+  const LayerW& last = e->layers.back();
+  const int pool_rows = c.pooling == MQ_POOL_CLS ? 1 : L;  // slab holds [B, H] CLS rows or [M, H]
+  hipLaunchKernelGGL((ln_pool_kernel<VPL>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, e->slab.p, dsplit,
+                     (int64_t)prev_rows * H, mask, B, L, pool_rows, c.pooling, last.ln2g, last.ln2b, eps, out);
+  e->tl.close(s);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+// The few-row forward serves B * L <= kRowsMax token rows (a single query up to 64
+// tokens); MQ_ROWS_PATH=0 turns it off (A/B measurements).
+bool use_rows_path(const mq_encoder* e, int B, int L) {
+  static const bool on = [] {
+    const char* v = getenv("MQ_ROWS_PATH");
+    return !(v && v[0] == '0');
+  }();
+  const mq_bert_config& c = e->cfg;
+  // slab holds the FFN-down planes: splits x rows x H floats
+  return on && (int64_t)B * L <= kRowsMax && !e->layers.empty() && c.ffn % 256 == 0 &&
+         rows_nb_ok(c.ffn / 256 / rows_splits(c.ffn)) &&
+         (size_t)rows_splits(c.ffn) * B * L * c.hidden <= e->slab.n;
+}
+
 }  // namespace
 
 namespace {
 
 int forward(mq_encoder* e, const int* ids, const int* mask, int B, int L, float* out,
             hipStream_t s) {
+  const bool rows = use_rows_path(e, B, L);
   switch (e->cfg.hidden) {
-    case 256: return forward_vpl<1>(e, ids, mask, B, L, out, s);
-    case 512: return forward_vpl<2>(e, ids, mask, B, L, out, s);
-    case 768: return forward_vpl<3>(e, ids, mask, B, L, out, s);
-    default: return forward_vpl<4>(e, ids, mask, B, L, out, s);
+    case 256: return rows ? forward_rows<1>(e, ids, mask, B, L, out, s) : forward_vpl<1>(e, ids, mask, B, L, out, s);
+    case 512: return rows ? forward_rows<2>(e, ids, mask, B, L, out, s) : forward_vpl<2>(e, ids, mask, B, L, out, s);
+    case 768: return rows ? forward_rows<3>(e, ids, mask, B, L, out, s) : forward_vpl<3>(e, ids, mask, B, L, out, s);
+    default: return rows ? forward_rows<4>(e, ids, mask, B, L, out, s) : forward_vpl<4>(e, ids, mask, B, L, out, s);
   }
 }
 

@@ -62,6 +62,43 @@ def test_shapes_vs_oracle(require_gpu, B, L, ragged, prec):
     _close(enc.embed(ids, mask), ref)
 
 
+@pytest.mark.parametrize("B,L,kw", [
+    (1, 32, {}), (1, 64, {}), (2, 32, {}), (3, 7, {}), (1, 1, {"layers": 1}),
+    (1, 5, {"pooling": POOL_MEAN}), (2, 16, {"pooling": POOL_MEAN}), (1, 32, {"gelu": GELU_TANH}),
+    (4, 16, {"layers": 3}),
+    (2, 20, {"hidden": 256, "heads": 4, "ffn": 512}), (1, 33, {"hidden": 512, "heads": 8, "ffn": 2048}),
+    (1, 24, {"hidden": 1024, "heads": 16, "ffn": 4096}),
+])
+def test_few_row_path_vs_oracle(require_gpu, B, L, kw):
+    """B * L <= 64 token rows take the few-row forward (K2r: one 16x16 output tile per
+    1024-thread workgroup over the full depth, LayerNorm applied while loading the next
+    GEMM's rows, ln_pool at the end); ragged masks on every sequence after the first."""
+    cfg = BertConfig(**{"layers": 2, **kw})
+    rng = np.random.default_rng(B * 100 + L)
+    ids = rng.integers(106, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    for b in range(1, B):
+        mask[b, int(rng.integers(1, L + 1)):] = 0
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    enc = Encoder(cfg)
+    _close(enc.embed(ids, mask), ref)
+
+
+def test_few_row_path_matches_tiled_path(require_gpu):
+    """The same sequences alone (few-row forward) and inside a 96-sequence batch (tiled
+    GEMMs): equal within fp32 reassociation."""
+    cfg = BertConfig(layers=3)
+    enc = Encoder(cfg)
+    rng = np.random.default_rng(11)
+    ids = rng.integers(106, cfg.vocab_size, (96, 32)).astype(np.int32)
+    mask = np.ones_like(ids)
+    mask[1::3, 20:] = 0
+    batch = enc.embed(ids, mask)
+    for b in (0, 1, 50, 95):
+        np.testing.assert_allclose(enc.embed(ids[b:b + 1], mask[b:b + 1])[0], batch[b], atol=1e-6)
+    np.testing.assert_allclose(enc.embed(ids[4:6], mask[4:6]), batch[4:6], atol=1e-6)
+
+
 def test_device_path_and_batch_invariance(require_gpu):
     import torch
     cfg = BertConfig(layers=2)
