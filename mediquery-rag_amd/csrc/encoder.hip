@@ -598,6 +598,110 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
   for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
 }
 
+// K3 for the few-row forward (L <= 64 keys, one sequence's latency): one 512-thread
+// workgroup per (sequence, head, 32-query tile).  Wave w = (key quarter kw = w >> 1,
+// query half qh = w & 1) computes its 16 x 16 block of S^T = K Q^T on
+// v_mfma_f32_16x16x4_f32 (dh = 64 in two 8-step chains), the softmax max and sum over
+// all keys are shared through LDS, and the wave multiplies its 16 keys' P^T (the S^T
+// accumulator is already the B operand) by V^T into a partial O^T; the four key
+// quarters' partials are summed in order.  Masking, scale and exp as attention_kernel;
+// the MFMA chain per SIMD is a quarter of the one-wave kernel's.
+__global__ __launch_bounds__(512) void attention_rows_kernel(const float* __restrict__ qkv,
+                                                             const int* __restrict__ mask, int L,
+                                                             int H, int heads, int q_tiles,
+                                                             float scale, float* __restrict__ ctx) {
+  __shared__ float smax[2][4][16], ssum[2][4][16];
+  __shared__ float opart[2][4][16][kDh + 1];  // [qh][kw][query][d]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kw = w >> 1, qh = w & 1;
+  const int c = lane & 15, g = lane >> 4;
+  const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
+  const int bseq = blockIdx.x / (q_tiles * heads);
+  const int64_t row0 = (int64_t)bseq * L;
+  const int ld = 3 * H;
+  const int q = qt * 32 + qh * 16 + c;  // this lane's query (B-operand column)
+  const int key = kw * 16 + c;          // this lane's key (A-operand row)
+
+  // operands: lane (c, g) holds d = 16 s + 4 g + t at MFMA step (s, t) in both
+  floatx4 qf[4], kf[4];
+  {
+    const float* qs = qkv + (row0 + min(q, L - 1)) * ld + h * kDh + 4 * g;
+    const float* ks = qkv + (row0 + min(key, L - 1)) * ld + H + h * kDh + 4 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const floatx4*>(qs + 16 * s) * scale;
+      kf[s] = *reinterpret_cast<const floatx4*>(ks + 16 * s);
+    }
+  }
+  // V^T operand of the PV step: d = 16 db + c, key = kw * 16 + 4 g + t
+  float vf[4][4];
+  {
+    const float* vs = qkv + row0 * ld + 2 * H + h * kDh + c;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kk = min(kw * 16 + 4 * g + t, L - 1);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) vf[db][t] = vs[(int64_t)kk * ld + 16 * db];
+    }
+  }
+  const bool kvalid = key < L && mask[row0 + min(key, L - 1)] != 0;
+  const unsigned kbits = (unsigned)(__ballot(kvalid) & 0xFFFFull);  // bit k: key kw*16+k usable
+
+  floatx4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s][t], qf[s][t], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s + 2][t], qf[s + 2][t], s1, 0, 0, 0);
+    }
+  // accumulator j = S^T[key kw*16 + 4g + j][query c]
+  floatx4 st = s0 + s1;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    st[j] = ((kbits >> (4 * g + j)) & 1u) ? st[j] : -INFINITY;
+    mx = fmaxf(mx, st[j]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  if (g == 0) smax[qh][kw][c] = mx;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(smax[qh][0][c], smax[qh][1][c]), fmaxf(smax[qh][2][c], smax[qh][3][c]));
+  float ls = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    st[j] = (st[j] == -INFINITY) ? 0.f : expf(st[j] - m);
+    ls += st[j];
+  }
+  ls += __shfl_xor(ls, 16);
+  ls += __shfl_xor(ls, 32);
+  if (g == 0) ssum[qh][kw][c] = ls;
+  floatx4 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    o[db] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[db][t], st[t], o[db], 0, 0, 0);
+  }
+  // o[db][j] = O^T[d = 16 db + 4 g + j][query c] over this wave's 16 keys
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) opart[qh][kw][c][16 * db + 4 * g + j] = o[db][j];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = e * 512 + (int)threadIdx.x;  // (query of the tile, d), d fastest
+    const int q32 = idx >> 6, d = idx & 63;
+    const int qq = q32 >> 4, qc = q32 & 15;
+    const float v = ((opart[qq][0][qc][d] + opart[qq][1][qc][d]) + opart[qq][2][qc][d]) + opart[qq][3][qc][d];
+    const float l = ((ssum[qq][0][qc] + ssum[qq][1][qc]) + ssum[qq][2][qc]) + ssum[qq][3][qc];
+    const int qrow = qt * 32 + q32;
+    if (qrow < L) ctx[(row0 + qrow) * H + h * kDh + d] = v * (l > 0.f ? 1.0f / l : 0.f);
+  }
+}
+
 // --------------------------------------------------------------- K7 pool -----
 // One wave per sequence: CLS row (or masked mean over rows), then x / max(||x||, 1e-12).
 template <int VPL>
@@ -1105,8 +1209,8 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     }
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
-    hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p);
+    hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
+                       H, c.heads, qt, scale, e->ctx.p);  // L <= kRowsMax = 64 keys
     e->tl.mark(s, ST_OPROJ);
     launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
     e->tl.mark(s, ST_FFN_UP);
