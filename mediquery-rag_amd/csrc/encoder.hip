@@ -476,20 +476,60 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
   ln_row_store<VPL>(x, g, b, eps, out + (int64_t)row * H, lane);
 }
 
-template <int VPL>
+// RPW rows per wave, loaded together and reduced with interleaved shuffle chains (the
+// per-row arithmetic is ln_row_store's, so results are bitwise those of one row per wave).
+template <int VPL, int RPW>
 __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, int M,
                                                  const float* __restrict__ g,
                                                  const float* __restrict__ b, float eps,
                                                  float* __restrict__ dst) {
   constexpr int H = VPL * 256;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  floatx4 x[VPL];
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= M) return;
+  floatx4 x[RPW][VPL];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i)
-    x[i] = *reinterpret_cast<const floatx4*>(src + (int64_t)row * H + (i * 64 + lane) * 4);
-  ln_row_store<VPL>(x, g, b, eps, dst + (int64_t)row * H, lane);
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+      x[r][i] = *reinterpret_cast<const floatx4*>(src + (int64_t)min(row0 + r, M - 1) * H + (i * 64 + lane) * 4);
+  float s[RPW], v[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    s[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) s[r] += x[r][i].x + x[r][i].y + x[r][i].z + x[r][i].w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) s[r] += __shfl_xor(s[r], off);
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float mean = s[r] * (1.0f / H);
+    v[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      x[r][i] -= mean;
+      v[r] += x[r][i].x * x[r][i].x + x[r][i].y * x[r][i].y + x[r][i].z * x[r][i].z + x[r][i].w * x[r][i].w;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) v[r] += __shfl_xor(v[r], off);
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    if (row0 + r >= M) break;
+    const float rstd = 1.0f / sqrtf(v[r] * (1.0f / H) + eps);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      const floatx4 gg = *reinterpret_cast<const floatx4*>(g + c);
+      const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c);
+      *reinterpret_cast<floatx4*>(dst + (int64_t)(row0 + r) * H + c) = x[r][i] * rstd * gg + bb;
+    }
+  }
 }
 
 // ------------------------------------------------------------ K3 attention ----
@@ -1039,7 +1079,18 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
   }
   gemm<EPI_RESID>(e, g, stage, s);
   e->tl.mark(s, ST_LN);
-  hipLaunchKernelGGL((ln_kernel<VPL>), dim3(rb), dim3(256), 0, s, g.out, g.M, lng, lnb, e->cfg.ln_eps, x);
+  static const int rpw = [] {  // rows per wave (A/B knob MQ_LN_RPW = 1 / 2 / 4)
+    const char* v = getenv("MQ_LN_RPW");
+    return v ? atoi(v) : 4;
+  }();
+  if (rpw == 4)
+    hipLaunchKernelGGL((ln_kernel<VPL, 4>), dim3((unsigned)((g.M + 15) / 16)), dim3(256), 0, s, g.out, g.M, lng,
+                       lnb, e->cfg.ln_eps, x);
+  else if (rpw == 1)
+    hipLaunchKernelGGL((ln_kernel<VPL, 1>), dim3(rb), dim3(256), 0, s, g.out, g.M, lng, lnb, e->cfg.ln_eps, x);
+  else
+    hipLaunchKernelGGL((ln_kernel<VPL, 2>), dim3((unsigned)((g.M + 7) / 8)), dim3(256), 0, s, g.out, g.M, lng,
+                       lnb, e->cfg.ln_eps, x);
 }
 
 // One forward.  With CLS pooling the last layer only needs the CLS rows after its
