@@ -345,7 +345,8 @@ __device__ __forceinline__ void ln_row_stats(const floatx4 (&x)[VPL], float eps,
 // store the normalised rows to ln_out: the residual input of the next projection.
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
-constexpr int kRowsMax = 64; // token rows up to which a forward takes this path
+constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
+constexpr int kRowsDefault = 64;  // ... and does by default (MQ_ROWS_MAX overrides)
 
 template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
 __global__ __launch_bounds__(1024) void rows_gemm_kernel(
@@ -1260,8 +1261,12 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     }
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
-    hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p);  // L <= kRowsMax = 64 keys
+    if (L <= 64)
+      hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
+                         H, c.heads, qt, scale, e->ctx.p);
+    else
+      hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L, H,
+                         c.heads, qt, scale, e->ctx.p);
     e->tl.mark(s, ST_OPROJ);
     launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
     e->tl.mark(s, ST_FFN_UP);
@@ -1289,13 +1294,15 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
 // The few-row forward serves B * L <= kRowsMax token rows (a single query up to 64
 // tokens); MQ_ROWS_PATH=0 turns it off (A/B measurements).
 bool use_rows_path(const mq_encoder* e, int B, int L) {
-  static const bool on = [] {
+  static const int rows_max = [] {
     const char* v = getenv("MQ_ROWS_PATH");
-    return !(v && v[0] == '0');
+    if (v && v[0] == '0') return 0;
+    const char* m = getenv("MQ_ROWS_MAX");
+    return m ? std::min(atoi(m), kRowsMax) : kRowsDefault;
   }();
   const mq_bert_config& c = e->cfg;
   // slab holds the FFN-down planes: splits x rows x H floats
-  return on && (int64_t)B * L <= kRowsMax && !e->layers.empty() && c.ffn % 256 == 0 &&
+  return (int64_t)B * L <= rows_max && !e->layers.empty() && c.ffn % 256 == 0 &&
          rows_nb_ok(c.ffn / 256 / rows_splits(c.ffn)) &&
          (size_t)rows_splits(c.ffn) * B * L * c.hidden <= e->slab.n;
 }

@@ -47,8 +47,21 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--exact-direct", action="store_true", help="search with MQ_DTYPE_F32 (default: the screen)")
+    ap.add_argument("--encoder-seq-lens", default="",
+                    help="comma list: only the single-query encoder p50 at these token counts")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if args.encoder_seq_lens:
+        enc = Encoder(DMETA_BASE, device=0)
+        q = torch.empty((1, 768), device=dev)
+        res = {}
+        for L in [int(x) for x in args.encoder_seq_lens.split(",")]:
+            ids_np, mask_np = synth.token_batch(1, L)
+            ids = torch.from_numpy(ids_np).to(dev)
+            mask = torch.from_numpy(mask_np).to(dev)
+            res["encoder_ms_L%d" % L] = p50(lambda: enc.embed_device(ids, mask, q), args.iters)
+        print(res, flush=True)
+        return
     corpus = synth.corpus_device(args.rows, 768, dev)
     ix = FlatIndex(dim=768, capacity=args.rows, device=0)
     ix.add_device(corpus)
