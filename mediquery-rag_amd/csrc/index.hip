@@ -983,6 +983,8 @@ struct mq_index {
   int64_t cap = 0;  // rows reserved
   float* rows = nullptr;  // [cap, dim], every stored row unit-norm
   int num_cus = 256;
+  int* host_flag = nullptr;  // pinned: the status word a search reads back (a pageable
+                             // 4-byte D2H copy is staged and costs more than the scan tail)
   DevBuf stage, cand_s, cand_i, out_s, out_i;
   DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
   int64_t n16 = 0;   // rows already mirrored into rows16
@@ -1141,6 +1143,15 @@ void launch_scan(const mq_index* ix, int kind, bool wide, const float* q, int nq
     launch_search<SearchNarrow, KC>(ix, q, nq, kl, G, nqt, cs, ci, s);
 }
 
+// Read a device status word back through the index's pinned host word (synchronises s).
+int read_flag(mq_index* ix, const int* dflag, hipStream_t s, int* out) {
+  if (!ix->host_flag) MQ_HIP(hipHostMalloc((void**)&ix->host_flag, sizeof(int), hipHostMallocDefault));
+  MQ_HIP(hipMemcpyAsync(ix->host_flag, dflag, sizeof(int), hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  *out = *ix->host_flag;
+  return MQ_OK;
+}
+
 // K9 fused scan + K10 merge -> exact top-k of the whole index for every query.
 // k <= 16 runs with lists of 8/16.  For 16 < k <= 64 the scan still keeps 16 per list
 // and the merge checks that no list overflowed (see merge_kernel); if one did, the
@@ -1196,8 +1207,8 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
     MQ_HIP(hipGetLastError());
     if (!flag) return MQ_OK;
     int overflow = 0;
-    MQ_HIP(hipMemcpyAsync(&overflow, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    MQ_HIP(hipStreamSynchronize(s));
+    rc = read_flag(ix, flag, s, &overflow);
+    if (rc) return rc;
     if (overflow & 1) {  // a scan list overflowed: re-scan with full-length lists
       ++ix->rescans;
       kc = MQ_MAX_K;
@@ -1432,8 +1443,8 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     MQ_HIP(hipGetLastError());
   }
   int n_fail = 0;
-  MQ_HIP(hipMemcpyAsync(&n_fail, ix->flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  MQ_HIP(hipStreamSynchronize(s));
+  rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);
+  if (rc) return rc;
   if (tier == TIER_I8) {
     // a corpus whose top scores crowd within the int8 bound fails most certificates: after
     // a run of failures the single-query path goes straight to the bf16 stream for a while
@@ -1556,6 +1567,7 @@ int mq_index_destroy(mq_index* ix) {
   {
     DeviceGuard dg(ix->device);
     if (ix->rows) (void)hipFree(ix->rows);
+    if (ix->host_flag) (void)hipHostFree(ix->host_flag);
     ix->stage.release();
     ix->cand_s.release();
     ix->cand_i.release();
