@@ -353,7 +353,9 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ A, int lda, int64_t a_plane, int M, const float* __restrict__ lng,
     const float* __restrict__ lnb, float eps, float* __restrict__ ln_out,
     const float* __restrict__ W, int ldw, const float* __restrict__ bias,
-    const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane) {
+    const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane,
+    const int* __restrict__ ids, int L, int vocab, const float* __restrict__ pos,
+    const float* __restrict__ typ) {
   constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
   // 16-deep blocks per load batch: all of them up to 12 (96 VGPRs of operands in flight,
   // one memory round trip), else batches of 8
@@ -381,18 +383,33 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   if (LN_IN) {
     const int row = r0 + wave;  // one wave per row (kRWaves == kRT)
     const float* src = A + (int64_t)min(row, M - 1) * lda;
-    // the row is the sum of S_IN split-K planes of the producing GEMM, added in order
-    floatx4 p[S_IN][VPL];
-#pragma unroll
-    for (int z = 0; z < S_IN; ++z)
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) p[z][i] = *reinterpret_cast<const floatx4*>(src + z * a_plane + (i * 64 + lane) * 4);
     floatx4 x[VPL];
+    if constexpr (S_IN == 0) {
+      // layer 0: the row is the embedding sum word[id] + pos[p] + type[0] (as
+      // embed_ln_kernel; A = the word table), normalised with the embedding LayerNorm
+      const int rr = min(row, M - 1);
+      int id = ids[rr];
+      id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      x[i] = p[0][i];
+      for (int i = 0; i < VPL; ++i) {
+        const int cc = (i * 64 + lane) * 4;
+        x[i] = *reinterpret_cast<const floatx4*>(A + (int64_t)id * K + cc) +
+               *reinterpret_cast<const floatx4*>(pos + (int64_t)(rr % L) * K + cc) +
+               *reinterpret_cast<const floatx4*>(typ + cc);
+      }
+    } else {
+      // the row is the sum of S_IN split-K planes of the producing GEMM, added in order
+      floatx4 p[S_IN][VPL];
 #pragma unroll
-      for (int z = 1; z < S_IN; ++z) x[i] += p[z][i];
+      for (int z = 0; z < S_IN; ++z)
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) p[z][i] = *reinterpret_cast<const floatx4*>(src + z * a_plane + (i * 64 + lane) * 4);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        x[i] = p[0][i];
+#pragma unroll
+        for (int z = 1; z < S_IN; ++z) x[i] += p[z][i];
+      }
     }
     float mu, rs;
     ln_row_stats<VPL>(x, eps, mu, rs);
@@ -1167,6 +1184,11 @@ struct RowsArgs {
   int64_t o_plane;  // floats between the output planes of a K split
   int M, N, K;      // K: full depth (ldw >= K)
   int splits;       // K splits (grid.z), each writing one output plane
+  // LN_IN with s_in = 0: A is the word-embedding table, rows gathered by token id
+  const int* ids = nullptr;
+  int L = 1, vocab = 0;
+  const float* pos = nullptr;
+  const float* typ = nullptr;
 };
 
 template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
@@ -1175,7 +1197,7 @@ void launch_rows_nb(const RowsArgs& g, const float* lng, const float* lnb, float
   hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN>),
                      dim3(g.N / kRT, (g.M + kRT - 1) / kRT, g.splits), dim3(64 * kRWaves), 0, s, g.A,
                      g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
-                     g.out, g.ldo, g.o_plane);
+                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ);
 }
 
 // Per-split depths the few-row kernel is instantiated for (K / 256 blocks per wave).
@@ -1209,11 +1231,13 @@ void launch_rows(const RowsArgs& g, hipStream_t s) {
   }
 }
 
-// A = LN(sum of s_in planes) with K == H, the normalised rows also to ln_out (may be null).
+// A = LN(sum of s_in planes) with K == H, the normalised rows also to ln_out (may be null);
+// s_in = 0: A = LN(embedding sum) gathered by token id (g.ids, g.pos, g.typ).
 template <int EPI, int VPL>
 void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* lnb, float eps,
                     float* ln_out, hipStream_t s) {
   switch (s_in) {
+    case 0: launch_rows_nb<EPI, true, VPL, VPL, 0>(g, lng, lnb, eps, ln_out, s); return;
     case 1: launch_rows_nb<EPI, true, VPL, VPL, 1>(g, lng, lnb, eps, ln_out, s); return;
     case 2: launch_rows_nb<EPI, true, VPL, VPL, 2>(g, lng, lnb, eps, ln_out, s); return;
     case 3: launch_rows_nb<EPI, true, VPL, VPL, 3>(g, lng, lnb, eps, ln_out, s); return;
@@ -1221,11 +1245,12 @@ void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* 
   }
 }
 
-// Few-row forward (B * L <= kRowsMax): 5 launches per layer instead of 9.  Between
+// Few-row forward (B * L <= kRowsMax): 5 launches per layer instead of 9, 5 L + 1 in all.  Between
 // layers the activations stay pre-LayerNorm, as the FFN-down's split-K planes in `slab`;
 // the next GEMM sums and normalises them on load (K2r LN_IN) and materialises the
 // normalised rows in x for the residual:
-//   QKV   qkv = LN2'(sum slab) Wqkv^T + b  (x = LN2'(...); layer 0 reads the embedding LN x)
+//   QKV   qkv = LN2'(sum slab) Wqkv^T + b  (x = LN2'(...); layer 0: LN of the gathered
+//         embedding sum, so the forward has no separate embedding launch)
 //   attn  ctx
 //   oproj y = ctx Wo^T + bo + x
 //   up    ffn = GELU(LN1(y) W1^T + b1)     (x = LN1(y))
@@ -1241,9 +1266,6 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
   const float scale = 1.0f / sqrtf((float)(H / c.heads));
   const int q_tiles = (L + 31) / 32;
   const int dsplit = rows_splits(F);
-  e->tl.mark(s, ST_EMBED);
-  hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, ids, M, L,
-                     c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, eps, e->x.p);
   int prev_rows = M;
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
@@ -1251,8 +1273,14 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;
     e->tl.mark(s, ST_QKV);
-    if (li == 0) {
-      launch_rows<EPI_BIAS>({e->x.p, H, 0, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1}, s);
+    if (li == 0) {  // the embedding gather + LayerNorm run inside the first QKV launch
+      RowsArgs g0{e->word, H, 0, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1};
+      g0.ids = ids;
+      g0.L = L;
+      g0.vocab = c.vocab_size;
+      g0.pos = e->pos;
+      g0.typ = e->typ;
+      launch_rows_ln<EPI_BIAS, VPL>(g0, 0, e->eg, e->eb, eps, e->x.p, s);
     } else {
       const LayerW& p = e->layers[li - 1];
       launch_rows_ln<EPI_BIAS, VPL>({e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p,
