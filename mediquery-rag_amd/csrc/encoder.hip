@@ -12,7 +12,9 @@
 //   K5 gemm (EPI_GELU)      FFN up + bias + GELU (erf or tanh)
 //   K6 gemm (EPI_RESID)     FFN down + bias + residual, then ln_kernel
 //   K7 pool_kernel          CLS / masked-mean pooling + L2 normalisation
-// All GEMMs run on the exact-fp32 MFMA core of gemm_f32.hpp.
+// All GEMMs run on the exact-fp32 MFMA core of gemm_f32.hpp (or its split-f32 form).
+// Few token rows (a single query, B * L <= 64) take forward_rows instead: 5 launches per
+// layer on the K2r / K3r kernels below, LayerNorm applied by the consuming GEMM.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
