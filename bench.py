@@ -300,6 +300,15 @@ def main():
                      "search_ms": round(statistics.median(srch_l), 3),
                      "search_tier": "int8 screen (K9q) -> fp32 re-rank + certificate",
                      "passdowns": index.screen_passdowns - pd0}
+        # one query's forward streams every fp32 weight matrix once (few-row path, 61
+        # launches): its HBM roofline is weights / 8 TB/s; the gap is per-launch latency
+        wbytes = 4 * cfg.layers * (4 * cfg.hidden * cfg.hidden + 2 * cfg.hidden * cfg.ffn)
+        enc_ms = lat_parts["encoder_ms"]
+        lat_parts["encoder_roofline"] = {
+            "bound": "hbm (weight streaming)", "weight_bytes": wbytes,
+            "achieved_gbs": round(wbytes / (enc_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+            "frac": round(wbytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "t_min_ms": round(wbytes / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}
         # the single query's scan: K9q sample + appending pass over the int8 shadow (HBM-bound)
         index.read_timing()
         index.set_timing(True)
