@@ -330,6 +330,46 @@ __device__ __forceinline__ void ln_row_stats(const floatx4 (&x)[VPL], float eps,
   rstd = 1.0f / sqrtf(wave_sum(v) * (1.0f / H) + eps);
 }
 
+// Wave sum with DPP lane moves inside each 16-lane row (xor 1, xor 2, half-row mirror, row
+// mirror) and two cross-row shuffles: 2 LDS-crossbar round trips instead of wave_sum's 6
+// (the few-row path's LayerNorm runs on the critical path of every launch).
+__device__ __forceinline__ float dpp_add(float v, int ctrl_id) {
+  int t;
+  switch (ctrl_id) {  // dpp_ctrl must be an immediate
+    case 0: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false); break;   // quad xor 1
+    case 1: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false); break;   // quad xor 2
+    case 2: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false); break;  // row half mirror
+    default: t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false); break; // row mirror
+  }
+  return v + __int_as_float(t);
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  v = dpp_add(v, 0);
+  v = dpp_add(v, 1);
+  v = dpp_add(v, 2);
+  v = dpp_add(v, 3);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+template <int VPL>
+__device__ __forceinline__ void ln_row_stats_fast(const floatx4 (&x)[VPL], float eps, float& mean,
+                                                  float& rstd) {
+  constexpr int H = VPL * 256;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += x[i].x + x[i].y + x[i].z + x[i].w;
+  mean = wave_sum_fast(s) * (1.0f / H);
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const floatx4 d = x[i] - mean;
+    v += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+  }
+  rstd = 1.0f / sqrtf(wave_sum_fast(v) * (1.0f / H) + eps);
+}
+
 // ------------------------------------------------------- few-row GEMM (K2r) ----
 // A single query is M = L <= 64 token rows: the tiled GEMM leaves the chip idle and the
 // split-K path pays a second launch for its ordered slab reduction (~5 us each, 4 per
@@ -345,6 +385,9 @@ __device__ __forceinline__ void ln_row_stats(const floatx4 (&x)[VPL], float eps,
 // first computes row r0 + w's mean / rstd (as ln_kernel) and A is normalised while it is
 // loaded, so no LayerNorm launch sits between the GEMMs.  The column-0 workgroups also
 // store the normalised rows to ln_out: the residual input of the next projection.
+#ifndef MQ_ROWS_DBG
+#define MQ_ROWS_DBG 0  // measurement builds only: 1 no weight loads, 2 no row loads, 4 no MFMA
+#endif
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
 constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
@@ -381,12 +424,16 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   // the first batch of weights is in flight before anything else (the LayerNorm pass
   // below waits on its own row loads only)
 #pragma unroll
-  for (int j = 0; j < CH; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+  for (int j = 0; j < CH; ++j)
+    wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : *reinterpret_cast<const floatx4*>(wrow + 16 * j);
   if (LN_IN) {
     const int row = r0 + wave;  // one wave per row (kRWaves == kRT)
     const float* src = A + (int64_t)min(row, M - 1) * lda;
     floatx4 x[VPL];
-    if constexpr (S_IN == 0) {
+    if constexpr (MQ_ROWS_DBG & 2) {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) x[i] = floatx4{0.1f * lane, 0.2f, 0.3f, 0.4f * wave};
+    } else if constexpr (S_IN == 0) {
       // layer 0: the row is the embedding sum word[id] + pos[p] + type[0] (as
       // embed_ln_kernel; A = the word table), normalised with the embedding LayerNorm
       const int rr = min(row, M - 1);
@@ -414,7 +461,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
       }
     }
     float mu, rs;
-    ln_row_stats<VPL>(x, eps, mu, rs);
+    ln_row_stats_fast<VPL>(x, eps, mu, rs);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int cc = (i * 64 + lane) * 4;
@@ -422,14 +469,17 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
              *reinterpret_cast<const floatx4*>(lnb + cc);
       *reinterpret_cast<floatx4*>(&arows[wave * AS + cc]) = x[i];
     }
-    if (ln_out && blockIdx.x == 0 && row < M) {
-#pragma unroll
-      for (int i = 0; i < VPL; ++i)
-        *reinterpret_cast<floatx4*>(ln_out + (int64_t)row * K + (i * 64 + lane) * 4) = x[i];
-    }
     // LDS-only barrier: the weight loads stay in flight across it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    // the normalised rows out, 16 columns per workgroup of this row tile (not all of
+    // them from one workgroup: the slowest workgroup sets the launch's duration)
+    if (ln_out && threadIdx.x < kRT * kRT) {
+      const int rr = threadIdx.x / kRT, cc = threadIdx.x % kRT;
+      if (r0 + rr < M)
+        for (int c0 = blockIdx.x * kRT; c0 < K; c0 += gridDim.x * kRT)
+          ln_out[(int64_t)(r0 + rr) * K + c0 + cc] = arows[rr * AS + c0 + cc];
+    }
   }
 
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -444,12 +494,18 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
       if (LN_IN)
         av[j] = *reinterpret_cast<const floatx4*>(&arows[c * AS + kb0 + 16 * (b + j) + 4 * kq]);
       else
-        av[j] = *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
+        av[j] = (MQ_ROWS_DBG & 2) ? floatx4{0.1f, 0.2f, 0.3f, 0.4f}
+                                  : *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
     }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], wv[j][t], acc, 0, 0, 0);
+      for (int t = 0; t < 4; ++t) {
+        if (MQ_ROWS_DBG & 4)
+          acc[t] += av[j][t] * wv[j][t];
+        else
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], wv[j][t], acc, 0, 0, 0);
+      }
     }
   }
   // accumulator element j is (row 4 kq + j, column c) of this wave's partial tile
