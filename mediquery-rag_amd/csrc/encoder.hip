@@ -623,25 +623,39 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
                                                        const int* __restrict__ mask, int L,
                                                        int H, int heads, int q_tiles,
                                                        float scale, float* __restrict__ ctx) {
-  __shared__ float obuf[32][kDh + 1];
+  // one LDS tile, used in turn to stage Q, each key tile's K, and the output: [32][68]
+  // rows for staging (a 16-lane ds_read_b128 group hits 16 distinct bank groups), [32][65]
+  // for the output
+  constexpr int kSt = kDh + 4;
+  __shared__ __attribute__((aligned(16))) float tile[32 * kSt];
+  float(*obuf)[kDh + 1] = reinterpret_cast<float(*)[kDh + 1]>(tile);
   const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
   const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
   const int bseq = blockIdx.x / (q_tiles * heads);
   const int q0 = qt * 32;
   const int64_t row0 = (int64_t)bseq * L;
   const int ld = 3 * H;
-
-  float qf[32];
-  {
-    const float* src = qkv + (row0 + min(q0 + r, L - 1)) * ld + h * kDh + hh * 32;
+  // Q / K tiles arrive by whole-line loads (4 rows x 256 B per wave-instruction) through
+  // LDS; read lane-strided straight from HBM (64 lines per instruction) the tiles were
+  // fetched ~2x (PMC), the lines evicted between the 8 instructions that share them.
+  auto stage = [&](int row_base, int col) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i) * scale;
-      qf[4 * i] = v.x;
-      qf[4 * i + 1] = v.y;
-      qf[4 * i + 2] = v.z;
-      qf[4 * i + 3] = v.w;
+      const int rr = 4 * i + (lane >> 4);
+      const float* src = qkv + (row0 + min(row_base + rr, L - 1)) * ld + col + (lane & 15) * 4;
+      *reinterpret_cast<floatx4*>(&tile[rr * kSt + (lane & 15) * 4]) = *reinterpret_cast<const floatx4*>(src);
     }
+  };
+
+  float qf[32];
+  stage(q0, h * kDh);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const floatx4 v = *reinterpret_cast<const floatx4*>(&tile[r * kSt + hh * 32 + 4 * i]) * scale;
+    qf[4 * i] = v.x;
+    qf[4 * i + 1] = v.y;
+    qf[4 * i + 2] = v.z;
+    qf[4 * i + 3] = v.w;
   }
   float m_run = -INFINITY, l_run = 0.f;
   floatx16 o0, o1;
@@ -653,16 +667,14 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
     const bool kvalid = (k0 + r < L) && mask[row0 + kr] != 0;
     const unsigned long long kbits = __ballot(kvalid);  // bit j = key k0 + j usable
     float kf[32];
-    {
-      const float* src = qkv + (row0 + kr) * ld + H + h * kDh + hh * 32;
+    stage(k0, H + h * kDh);  // (one wave: its LDS reads of the last tile precede these writes)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(src + 4 * i);
-        kf[4 * i] = v.x;
-        kf[4 * i + 1] = v.y;
-        kf[4 * i + 2] = v.z;
-        kf[4 * i + 3] = v.w;
-      }
+    for (int i = 0; i < 8; ++i) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(&tile[r * kSt + hh * 32 + 4 * i]);
+      kf[4 * i] = v.x;
+      kf[4 * i + 1] = v.y;
+      kf[4 * i + 2] = v.z;
+      kf[4 * i + 3] = v.w;
     }
     floatx16 st;
 #pragma unroll
