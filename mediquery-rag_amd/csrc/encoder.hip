@@ -1271,14 +1271,21 @@ void launch_rows_nb(const RowsArgs& g, const float* lng, const float* lnb, float
 }
 
 // Per-split depths the few-row kernel is instantiated for (K / 256 blocks per wave).
-bool rows_nb_ok(int nb) { return nb >= 1 && (nb <= 4 || nb == 8 || nb == 12 || nb == 16); }
+bool rows_nb_ok(int nb) { return nb >= 1 && (nb <= 4 || nb == 6 || nb == 8 || nb == 12 || nb == 16); }
 
-// K splits for a depth-K projection: per-split depth <= 1024 (more workgroups pull the
-// weights: at K = 3072 one split is 13.9 us, three 128 KB splits are cheaper even with
-// the planes summed by the consumer), at most 4.
+// K splits for a depth-K projection: the fewest with per-split depth <= 1536, at most 4.
+// More splits put more workgroups on the weights but add planes the consumer sums (at
+// K = 3072, encoder p50: one split 13.9 us per FFN-down launch; two 0.474 ms, three 0.495,
+// four 0.493 - FFN-down 8.9 / 9.2 / 7.1 us, the next QKV 9.2 / 10.0 / 11.0 us).
 int rows_splits(int K) {
   const int nb = K / 256;
-  if (nb > 4 && nb % 4 == 0 && nb / 4 <= 4) return nb / 4;
+  static const int forced = [] {  // A/B knob MQ_ROWS_SPLITS (used when it divides K / 256)
+    const char* v = getenv("MQ_ROWS_SPLITS");
+    return v ? atoi(v) : 0;
+  }();
+  if (forced >= 1 && forced <= 4 && nb % forced == 0 && rows_nb_ok(nb / forced)) return forced;
+  for (int sp = 1; sp <= 4; ++sp)
+    if (nb % sp == 0 && nb / sp <= 6 && rows_nb_ok(nb / sp)) return sp;
   return 1;
 }
 
@@ -1295,6 +1302,7 @@ void launch_rows(const RowsArgs& g, hipStream_t s) {
     case 2: launch_rows_plain<EPI, 2>(g, s); return;
     case 3: launch_rows_plain<EPI, 3>(g, s); return;
     case 4: launch_rows_plain<EPI, 4>(g, s); return;
+    case 6: launch_rows_plain<EPI, 6>(g, s); return;
     case 8: launch_rows_plain<EPI, 8>(g, s); return;
     case 12: launch_rows_plain<EPI, 12>(g, s); return;
     default: launch_rows_plain<EPI, 16>(g, s); return;
