@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--single-iters", type=int, default=50, help="single-query latency samples")
     p.add_argument("--secondary-seq-len", type=int, default=128,
                    help="also time the headline step at this L (0 = skip)")
+    p.add_argument("--config4-steps", type=int, default=10,
+                   help="BASELINE config 4 line (10M x 768 as 8 row shards, batch 1024): timed steps (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     return p.parse_args()
@@ -73,8 +75,10 @@ def encoder_flops(cfg, B, L):
 
 
 def cpu_baseline(args, cfg, corpus_host_fn):
-    """Oracle (torch-CPU restatement) timed on this host: encoder on 2 batches of
-    `batch` queries + fp32 mm/topk over the full corpus for 1 batch."""
+    """Oracle (torch-CPU restatement) timed on this host: q/s = batch /
+    (median of 5 encoder batches + median of 5 fp32 mm/topk batches over the full
+    corpus), after one warm-up batch each; p50 single query = median over 20 single
+    queries of encoder + search (bounded: ~20 s of CPU work in all)."""
     from oracle.encoder import OracleEncoder
     from oracle.flat import search_fp32_torch
     from mediquery_hip.weights import synthetic_state_dict
@@ -82,23 +86,127 @@ def cpu_baseline(args, cfg, corpus_host_fn):
     torch.set_num_threads(threads)
     enc = OracleEncoder(cfg, synthetic_state_dict(cfg, 0))
     ids, mask = synth.token_batch(args.batch, args.seq_len)
-    enc.embed(ids[:8], mask[:8])  # warm-up
-    t0 = time.perf_counter()
-    reps = 2
+    reps, singles = 5, 20
+    q = enc.embed(ids, mask)  # warm-up batch
+    t_enc = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         q = enc.embed(ids, mask)
-    t_enc = (time.perf_counter() - t0) / reps
+        t_enc.append(time.perf_counter() - t0)
     c = corpus_host_fn()
-    search_fp32_torch(q[:4], c[:1000], args.k, threads)  # warm-up
-    t0 = time.perf_counter()
-    search_fp32_torch(q, c, args.k, threads)
-    t_search = time.perf_counter() - t0
-    return {"value": round(args.batch / (t_enc + t_search), 2), "unit": "queries/s",
+    search_fp32_torch(q, c, args.k, threads)  # warm-up batch
+    t_search = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        search_fp32_torch(q, c, args.k, threads)
+        t_search.append(time.perf_counter() - t0)
+    lat = []
+    for j in range(singles + 2):
+        t0 = time.perf_counter()
+        q1 = enc.embed(ids[j:j + 1], mask[j:j + 1])
+        search_fp32_torch(q1, c, args.k, threads)
+        if j >= 2:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    te, ts = statistics.median(t_enc), statistics.median(t_search)
+    return {"value": round(args.batch / (te + ts), 2), "unit": "queries/s",
             "cores": threads, "kind": "port",
-            "sample": ("oracle torch-CPU fp32: %d x %d-layer BERT encodes of %d queries (L=%d) "
-                       "+ 1 fp32 mm+topk of %d queries over %d x 768 rows; enc %.3f s/batch, "
-                       "search %.3f s/batch" % (reps, cfg.layers, args.batch, args.seq_len,
-                                                args.batch, c.shape[0], t_enc, t_search))}
+            "p50_single_query_ms": round(statistics.median(lat), 2),
+            "sample": ("oracle torch-CPU fp32 on %d threads: median of %d %d-layer BERT encodes of %d "
+                       "queries (L=%d) + median of %d fp32 mm+topk batches of %d queries over %d x 768 "
+                       "rows (enc %.3f s/batch, search %.3f s/batch); p50 of %d single queries "
+                       "(encode + search)" % (threads, reps, cfg.layers, args.batch, args.seq_len, reps,
+                                              args.batch, c.shape[0], te, ts, singles))}
+
+
+C4_ROWS, C4_SHARDS, C4_BATCH = 10_000_000, 8, 1024
+
+
+def config4(args, enc, world, rank, dev, backend):
+    """BASELINE config 4: a 10M x 768 fp32 corpus in 8 row shards of 1.25M, batch 1024
+    (global), k = 5.  Rank r of N owns shards [r*8/N, (r+1)*8/N) as `LocalShards` (all 8 on
+    one GPU at N = 1), embeds 1024/N of the queries (DP), and the ranks exchange query
+    embeddings and the packed per-shard candidates with one all-gather each.  Total work
+    is fixed as N grows ("strong").  Returns the rank's record (rank 0's is printed)."""
+    from mediquery_hip.distributed import LocalShards
+    if C4_SHARDS % world or C4_BATCH % world:
+        return None
+    spr, per = C4_SHARDS // world, C4_ROWS // C4_SHARDS
+    first = rank * spr
+    block = torch.empty((spr * per, 768), dtype=torch.float32, device=dev)
+    for j in range(spr):
+        block[j * per:(j + 1) * per] = synth.corpus_shard_device(per, first + j, 768, dev)
+    shards = LocalShards(spr, 768, device=dev.index)
+    shards.add_device(block)
+    del block
+    shards.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    B = C4_BATCH // world
+    K = args.k
+    ids_np, mask_np = synth.token_batch(B, args.seq_len, seed=synth.TOKEN_SEED + 100 + rank)
+    ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
+    q = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    s_loc = torch.empty((C4_BATCH, K), dtype=torch.float32, device=dev)
+    i_loc = torch.empty((C4_BATCH, K), dtype=torch.int64, device=dev)
+
+    def local(qq, k):
+        n = qq.shape[0]
+        shards.search_device(qq, k, s_loc[:n], i_loc[:n])
+        return s_loc[:n], i_loc[:n]
+
+    searcher = ShardedSearcher(local, first * per)
+    # property check at full size: queries planted on shard 0's rows (regenerated on every
+    # rank, so the query set is identical everywhere) find their global row ids
+    sh0 = synth.corpus_shard_device(per, 0, 768, dev)
+    pq, planted = synth.queries_device(64, sh0)
+    del sh0
+    torch.cuda.empty_cache()
+    _, pi = searcher.search(pq, K) if world > 1 else local(pq, K)
+    ok = bool((pi[:32, 0] == planted[:32]).all())
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        enc.embed_device(ids, mask, q)
+        if ev:
+            ev[1].record()
+        if world > 1:
+            searcher.search_local_batch(q, K, sizes=[B] * world)
+        else:
+            local(q, K)
+        if ev:
+            ev[2].record()
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.config4_steps)]
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(args.config4_steps):
+        step(evs[it])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    fb = sum(ix.screen_fallbacks for ix in shards.shards)
+    del shards
+    torch.cuda.empty_cache()
+    return {"workload": "BASELINE config 4: %d x 768 fp32 corpus as %d row shards of %d (%d per GPU x %d GPU), "
+                        "batch %d (global, %d per GPU, L=%d) embed + exact top-%d, one packed candidate "
+                        "all-gather%s" % (C4_ROWS, C4_SHARDS, per, spr, world, C4_BATCH, B, args.seq_len, K,
+                                          "" if world > 1 else " (none needed: device merge of the 8 shards)"),
+            "queries_per_s": round(C4_BATCH * args.config4_steps / elapsed, 1),
+            "ms_per_step": round(elapsed / args.config4_steps * 1e3, 3),
+            "steps": args.config4_steps, "n_gpus": world, "scaling": "strong",
+            "encoder_ms": round(statistics.mean(e[0].elapsed_time(e[1]) for e in evs), 3),
+            "search_ms": round(statistics.mean(e[1].elapsed_time(e[2]) for e in evs), 3),
+            "planted_top1_ok": ok, "screen_fallbacks": fb}
 
 
 def workload_name(rows, batch, world):
@@ -324,6 +432,8 @@ def main():
                        "traffic": (traffic_db_early.get("i8_thresh_kernel", 0) + traffic_db_early.get("i8_thresh_sample", 0))
                        or None}
 
+    c4 = config4(args, enc, world, rank, dev, backend) if args.config4_steps > 0 else None
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -431,6 +541,7 @@ def main():
             kk: alt_s[kk] for kk in ("value", "ms_per_step", "encoder_ms", "search_ms", "roofline",
                                      "planted_top1_ok", "screen_fallbacks", "screen_passdowns")},
     }
+    out["config4_sharded"] = c4
     out["config5_bf16_rerank"] = cfg5
     out["secondary_long_queries"] = sec
     if world == 1 and not args.no_cpu_baseline:

@@ -4,10 +4,13 @@
 // forward (reference src/medical_engine.py:43).  This is the
 // native restatement of mediquery_hip/tokenizer.py (the Python twin is the parity
 // oracle for it):
-//   * WordPiece: BERT basic tokenisation (drop control chars, split on whitespace,
-//     isolate CJK ideographs and punctuation, lower-case + strip combining marks) and
-//     greedy longest-match-first WordPiece over a local vocab.txt ("##" continuations,
-//     [UNK] for unmatched words and words over 100 code points).
+//   * WordPiece as the published BERT tokenizer computes it (the `tokenizers` crate's
+//     BertNormalizer + BertPreTokenizer + WordPiece = transformers.BertTokenizer; pinned
+//     by tests/golden/wordpiece_golden.json): drop NUL / U+FFFD / Cc Cf Co Cs except
+//     \t \n \r, isolate CJK ideographs, uncased: NFD + drop Mn + per-character lower-case
+//     mapping, then split on whitespace and isolate punctuation (ASCII symbols or P*), and
+//     greedy longest-match-first WordPiece over the vocab ("##" continuations, [UNK] for
+//     unmatched words and words over 100 code points).
 //   * Char: one id per non-space code point, 106 + crc32(utf-8 bytes) % (vocab - 106).
 // Both frame sequences as [CLS] ... [SEP], truncate to max_length and right-pad with 0.
 #include <cstdint>
@@ -87,143 +90,96 @@ void encode_utf8(uint32_t c, std::string& out) {
 }
 
 // ----------------------------------------------------- character classes -----
-// Python str.isspace(): Unicode White_Space plus the ASCII separators.
+// Unicode data generated from Python's unicodedata by tools/gen_unicode_tables.py.
+struct CpRange {
+  uint32_t lo, hi;
+};
+struct CpMap4 {
+  uint32_t cp, to[4];
+};
+struct CpMap3 {
+  uint32_t cp, to[3];
+};
+#include "unicode_tables.inc"
+
+template <size_t N>
+bool in_ranges(const CpRange (&t)[N], uint32_t c) {
+  size_t lo = 0, hi = N;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (t[mid].hi < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < N && t[lo].lo <= c;
+}
+
+template <class M, size_t N>
+const M* find_map(const M (&t)[N], uint32_t c) {
+  size_t lo = 0, hi = N;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (t[mid].cp < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < N && t[lo].cp == c ? &t[lo] : nullptr;
+}
+
+// White_Space (Python str.isspace() adds U+001C..U+001F, which are controls and dropped
+// before this test is reached).
 bool is_space(uint32_t c) {
   return c == ' ' || (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x1F) || c == 0x85 ||
          c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 ||
          c == 0x202F || c == 0x205F || c == 0x3000;
 }
 
+// The tokenizers crate's CJK table (its fourth extension range starts at 0x2B920).
 bool is_cjk(uint32_t c) {
   return (c >= 0x4E00 && c <= 0x9FFF) || (c >= 0x3400 && c <= 0x4DBF) ||
-         (c >= 0x20000 && c <= 0x2A6DF) || (c >= 0x2A700 && c <= 0x2CEAF) ||
+         (c >= 0x20000 && c <= 0x2A6DF) || (c >= 0x2A700 && c <= 0x2B73F) ||
+         (c >= 0x2B740 && c <= 0x2B81F) || (c >= 0x2B920 && c <= 0x2CEAF) ||
          (c >= 0xF900 && c <= 0xFAFF) || (c >= 0x2F800 && c <= 0x2FA1F);
 }
 
-// BERT's punctuation test: ASCII symbol ranges, or Unicode category P* (the ranges
-// below cover the P* code points of the BMP blocks the corpus uses: Latin-1, General
-// Punctuation, CJK Symbols, Fullwidth/Halfwidth Forms, CJK Compatibility Forms).
+// BERT's punctuation test: ASCII symbol ranges, or general category P*.
 bool is_punct(uint32_t c) {
   if ((c >= 33 && c <= 47) || (c >= 58 && c <= 64) || (c >= 91 && c <= 96) || (c >= 123 && c <= 126))
     return true;
-  if (c == 0xA1 || c == 0xA7 || c == 0xAB || c == 0xB6 || c == 0xB7 || c == 0xBB || c == 0xBF ||
-      c == 0x37E || c == 0x387)
-    return true;
-  if (c >= 0x2010 && c <= 0x2027) return true;
-  if (c >= 0x2030 && c <= 0x2043) return true;
-  if (c >= 0x2045 && c <= 0x2051) return true;
-  if (c >= 0x2053 && c <= 0x205E) return true;
-  if (c == 0x207D || c == 0x207E || c == 0x208D || c == 0x208E) return true;
-  if (c >= 0x2308 && c <= 0x230B) return true;
-  if (c == 0x2329 || c == 0x232A) return true;
-  if (c >= 0x2768 && c <= 0x2775) return true;
-  if (c >= 0x27C5 && c <= 0x27C6) return true;
-  if (c >= 0x27E6 && c <= 0x27EF) return true;
-  if (c >= 0x2E00 && c <= 0x2E4F) return true;
-  if (c >= 0x3001 && c <= 0x3003) return true;
-  if (c >= 0x3008 && c <= 0x3011) return true;
-  if (c >= 0x3014 && c <= 0x301F) return true;
-  if (c == 0x3030 || c == 0x303D || c == 0x30A0 || c == 0x30FB) return true;
-  if (c >= 0xFE10 && c <= 0xFE19) return true;
-  if (c >= 0xFE30 && c <= 0xFE52) return true;
-  if (c >= 0xFE54 && c <= 0xFE61) return true;
-  if (c == 0xFE63 || c == 0xFE68 || c == 0xFE6A || c == 0xFE6B) return true;
-  if ((c >= 0xFF01 && c <= 0xFF03) || (c >= 0xFF05 && c <= 0xFF0A) || (c >= 0xFF0C && c <= 0xFF0F))
-    return true;
-  if (c == 0xFF1A || c == 0xFF1B || c == 0xFF1F || c == 0xFF20) return true;
-  if ((c >= 0xFF3B && c <= 0xFF3D) || c == 0xFF3F || c == 0xFF5B || c == 0xFF5D) return true;
-  if (c >= 0xFF5F && c <= 0xFF65) return true;
-  return false;
+  return in_ranges(kPunct, c);
 }
 
-// category Cc / Cf (dropped by the basic tokeniser unless \t \n \r)
+// Dropped by the clean-up: categories Cc / Cf / Co / Cs except \t \n \r.
 bool is_control(uint32_t c) {
   if (c == '\t' || c == '\n' || c == '\r') return false;
-  if (c < 0x20 || (c >= 0x7F && c <= 0x9F)) return true;
-  return c == 0xAD || (c >= 0x600 && c <= 0x605) || c == 0x61C || c == 0x6DD || c == 0x70F ||
-         c == 0x180E || (c >= 0x200B && c <= 0x200F) || (c >= 0x202A && c <= 0x202E) ||
-         (c >= 0x2060 && c <= 0x2064) || (c >= 0x2066 && c <= 0x206F) || c == 0xFEFF ||
-         (c >= 0xFFF9 && c <= 0xFFFB);
+  return in_ranges(kOther, c);
 }
 
-bool is_combining_mark(uint32_t c) {  // category Mn in the ranges lower-casing can produce
-  return (c >= 0x300 && c <= 0x36F) || (c >= 0x1AB0 && c <= 0x1AFF) ||
-         (c >= 0x1DC0 && c <= 0x1DFF) || (c >= 0x20D0 && c <= 0x20FF) || (c >= 0xFE20 && c <= 0xFE2F);
-}
-
-// lower-case + NFD accent strip (Python: NFD(lower(c)) minus category Mn) for ASCII,
-// Latin-1, Greek / Cyrillic capitals and fullwidth Latin; other code points unchanged.
+// Uncased normalisation of one code point: NFD (Hangul syllables algorithmically), drop
+// category Mn, then each remaining character's full lower-case mapping.
 void lower_strip(uint32_t c, std::vector<uint32_t>& out) {
-  if (c >= 'A' && c <= 'Z') {
-    out.push_back(c + 32);
-    return;
+  uint32_t d[4] = {c, 0, 0, 0};
+  int nd = 1;
+  if (c >= 0xAC00 && c <= 0xD7A3) {  // Hangul syllable -> L V (T) jamo
+    const uint32_t s = c - 0xAC00;
+    d[0] = 0x1100 + s / 588;
+    d[1] = 0x1161 + (s % 588) / 28;
+    nd = 2;
+    if (s % 28) d[nd++] = 0x11A7 + s % 28;
+  } else if (const CpMap4* m = find_map(kNfd, c)) {
+    nd = 0;
+    for (int i = 0; i < 4 && m->to[i]; ++i) d[nd++] = m->to[i];
   }
-  if (c >= 0xC0 && c <= 0xFF) {
-    // base letter of each Latin-1 letter after NFD; '.' = keep the (lower-cased) char
-    static const char kBase[65] =
-        "aaaaaa.ceeeeiiii.nooooo..uuuuy.."   // C0..DF
-        "aaaaaa.ceeeeiiii.nooooo..uuuuy.y";  // E0..FF
-    const char b = kBase[c - 0xC0];
-    if (b != '.') {
-      out.push_back((uint32_t)b);
-    } else if (c == 0xD7 || c == 0xF7 || c == 0xDF) {
-      out.push_back(c);  // × ÷ ß
+  for (int i = 0; i < nd; ++i) {
+    if (in_ranges(kMn, d[i])) continue;
+    if (const CpMap3* l = find_map(kLower, d[i])) {
+      for (int j = 0; j < 3 && l->to[j]; ++j) out.push_back(l->to[j]);
     } else {
-      out.push_back(c <= 0xDE ? c + 32 : c);  // Æ Ð Ø Þ -> æ ð ø þ
+      out.push_back(d[i]);
     }
-    return;
   }
-  if (c >= 0x100 && c <= 0x17F) {  // Latin Extended-A
-    static const char kBaseA[129] =
-        "aaaaaaccccccccdd"   // 100-10F
-        "..eeeeeeeeeegggg"   // 110-11F
-        "gggghh..iiiiiiii"   // 120-12F
-        "!...jjkk.llllll."   // 130-13F
-        "...nnnnnn...oooo"   // 140-14F
-        "oo..rrrrrrssssss"   // 150-15F
-        "sstttt..uuuuuuuu"   // 160-16F
-        "uuuuwwyyyzzzzzz.";  // 170-17F
-    const char b = kBaseA[c - 0x100];
-    if (b == '!') {
-      out.push_back('i');  // İ -> i + U+0307 -> i
-    } else if (b != '.') {
-      out.push_back((uint32_t)b);
-    } else if (c == 0x138 || c == 0x149 || c == 0x17F) {
-      out.push_back(c);  // ĸ ŉ ſ
-    } else if (c >= 0x139 && c <= 0x148) {
-      out.push_back((c & 1) ? c + 1 : c);  // odd capitals in this stretch
-    } else {
-      out.push_back((c & 1) ? c : c + 1);
-    }
-    return;
-  }
-  switch (c) {  // Greek with tonos / dialytika -> base letter
-    case 0x386: case 0x3AC: out.push_back(0x3B1); return;
-    case 0x388: case 0x3AD: out.push_back(0x3B5); return;
-    case 0x389: case 0x3AE: out.push_back(0x3B7); return;
-    case 0x38A: case 0x3AF: case 0x390: case 0x3AA: case 0x3CA: out.push_back(0x3B9); return;
-    case 0x38C: case 0x3CC: out.push_back(0x3BF); return;
-    case 0x38E: case 0x3CD: case 0x3B0: case 0x3AB: case 0x3CB: out.push_back(0x3C5); return;
-    case 0x38F: case 0x3CE: out.push_back(0x3C9); return;
-    // Cyrillic letters with a combining mark in NFD -> base letter
-    case 0x400: case 0x401: case 0x450: case 0x451: out.push_back(0x435); return;
-    case 0x403: case 0x453: out.push_back(0x433); return;
-    case 0x407: case 0x457: out.push_back(0x456); return;
-    case 0x40C: case 0x45C: out.push_back(0x43A); return;
-    case 0x40D: case 0x45D: case 0x419: case 0x439: out.push_back(0x438); return;
-    case 0x40E: case 0x45E: out.push_back(0x443); return;
-    default: break;
-  }
-  if (c >= 0x400 && c <= 0x40F) {  // remaining Cyrillic capitals of the 0x450 row
-    out.push_back(c + 80);
-    return;
-  }
-  if ((c >= 0x391 && c <= 0x3A9 && c != 0x3A2) || (c >= 0x410 && c <= 0x42F) ||
-      (c >= 0xFF21 && c <= 0xFF3A)) {
-    out.push_back(c + 32);  // Greek / Cyrillic / fullwidth capitals
-    return;
-  }
-  out.push_back(c);
 }
 
 uint32_t crc32_bytes(const std::string& s) {
@@ -256,9 +212,11 @@ struct mq_tokenizer {
   }
 
   void wordpiece_ids(const std::vector<uint32_t>& cps, std::vector<int>& body) const {
-    // basic tokenisation into words (vectors of code points)
+    // basic tokenisation into words (vectors of normalised code points): clean-up, CJK
+    // isolation, per-character normalisation, then whitespace / punctuation splits on the
+    // normalised characters (the BertNormalizer -> BertPreTokenizer order)
     std::vector<std::vector<uint32_t>> words;
-    std::vector<uint32_t> cur;
+    std::vector<uint32_t> cur, norm;
     auto flush = [&]() {
       if (!cur.empty()) words.push_back(cur);
       cur.clear();
@@ -267,26 +225,30 @@ struct mq_tokenizer {
       if (c == 0 || c == 0xFFFD || is_control(c)) continue;
       if (is_space(c)) {
         flush();
-      } else if (is_cjk(c) || is_punct(c)) {
+        continue;
+      }
+      norm.clear();
+      if (lower)
+        lower_strip(c, norm);
+      else
+        norm.push_back(c);
+      if (is_cjk(c)) {
         flush();
-        words.push_back({c});
-      } else {
-        cur.push_back(c);
+        words.push_back(norm);
+        continue;
+      }
+      for (uint32_t n : norm) {
+        if (is_punct(n)) {
+          flush();
+          words.push_back({n});
+        } else {
+          cur.push_back(n);
+        }
       }
     }
     flush();
     std::string piece;
-    for (auto& w : words) {
-      std::vector<uint32_t> lw;
-      if (lower) {
-        for (uint32_t c : w) lower_strip(c, lw);
-        std::vector<uint32_t> kept;
-        for (uint32_t c : lw)
-          if (!is_combining_mark(c)) kept.push_back(c);
-        lw.swap(kept);
-      } else {
-        lw = w;
-      }
+    for (auto& lw : words) {
       if (lw.empty()) continue;
       if (lw.size() > 100) {
         body.push_back(unk);

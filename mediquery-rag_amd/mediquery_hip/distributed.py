@@ -5,15 +5,20 @@ a contiguous block of rows [offset_r, offset_r + n_r); global row id = offset_r 
 id.  A search is:
   1. (optional) all-gather of the ranks' query embeddings  -> every rank holds all queries
   2. local exact top-k on the rank's shard                  (K9/K10 on the device)
-  3. ONE all-gather of the per-shard [nq, k] (score, id) candidates
+  3. ONE all-gather of the per-shard [nq, k] (score, id) candidates, packed into a single
+     int32 [nq, k, 3] tensor (score bits, id low word, id high word)
   4. merge to the global top-k by (score desc, global id asc)  (device K10 or host merge)
 Scoring needs no communication; the exchanged bytes are nq*k*12 per rank.
+
+`LocalShards` is the same partition held as several shards on ONE device (BASELINE
+config 4's 8 shards on fewer GPUs than shards): per-shard K9 searches, then the device
+merge (K10) - the exchange step without the collective.
 """
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from .native import merge_topk_device, merge_topk_host
+from .native import FlatIndex, merge_topk_device, merge_topk_host
 
 
 def shard_bounds(n_rows, world, rank):
@@ -21,6 +26,75 @@ def shard_bounds(n_rows, world, rank):
     base, extra = divmod(n_rows, world)
     off = rank * base + min(rank, extra)
     return off, base + (1 if rank < extra else 0)
+
+
+def pack_candidates(scores, ids):
+    """(scores [nq, k] f32, ids [nq, k] int64) -> one int32 [nq, k, 3] tensor, so the
+    candidate exchange is a single collective: word 0 = the score's bits, words 1-2 =
+    the id (little-endian halves)."""
+    nq, k = scores.shape
+    packed = torch.empty((nq, k, 3), dtype=torch.int32, device=scores.device)
+    packed[..., 0] = scores.contiguous().view(torch.int32)
+    packed[..., 1:] = ids.contiguous().view(torch.int32).view(nq, k, 2)
+    return packed
+
+
+def unpack_candidates(packed):
+    """[..., k, 3] int32 -> (scores [..., k] f32, ids [..., k] int64)."""
+    s = packed[..., 0].contiguous().view(torch.float32)
+    i = packed[..., 1:].contiguous().view(torch.int64).squeeze(-1)
+    return s, i
+
+
+class LocalShards:
+    """Row shards of one corpus held as separate `FlatIndex` handles on ONE device
+    (BASELINE config 4's 8-shard partition when a rank owns several shards; the
+    reference store being scaled is the Chroma collection of src/medical_engine.py:52).
+    Shard s holds rows `shard_bounds(n, n_shards, s)` of what `add_device` receives
+    (global id = `base` + shard offset + local id); a search runs K9 on every shard into
+    one [n_shards, nq, k] candidate buffer and merges it on the device (K10)."""
+
+    def __init__(self, n_shards, dim=768, device=0, base=0):
+        self.n_shards, self.dim, self.device, self.base = int(n_shards), dim, device, int(base)
+        self.shards = [FlatIndex(dim=dim, device=device) for _ in range(self.n_shards)]
+        self.offsets = [0] * self.n_shards
+        self._cand = None
+
+    def __len__(self):
+        return sum(len(s) for s in self.shards)
+
+    def add_device(self, rows):
+        """Partition `rows` [n, dim] (torch, device) into the shards (empty shards only)."""
+        if len(self):
+            raise ValueError("LocalShards holds rows already: partition once")
+        n = int(rows.shape[0])
+        for s in range(self.n_shards):
+            off, cnt = shard_bounds(n, self.n_shards, s)
+            self.offsets[s] = off
+            if cnt:  # sized to the shard up front: no re-allocation while adding
+                self.shards[s] = FlatIndex(dim=self.dim, capacity=cnt, device=self.device)
+                self.shards[s].add_device(rows[off:off + cnt].contiguous())
+
+    def set_precision(self, dtype):
+        for ix in self.shards:
+            ix.set_precision(dtype)
+
+    def search_device(self, queries, k, out_scores, out_ids):
+        """Global top-k of `queries` [nq, dim] over every shard into out_scores [nq, k] f32
+        / out_ids [nq, k] int64 (ids global: base + shard offset + local row)."""
+        nq = int(queries.shape[0])
+        shape = (self.n_shards, nq, k)
+        if self._cand is None or self._cand[0].shape != shape:
+            dev = queries.device
+            offs = torch.tensor([self.base + o for o in self.offsets], dtype=torch.int64, device=dev)
+            self._cand = (torch.empty(shape, dtype=torch.float32, device=dev),
+                          torch.empty(shape, dtype=torch.int64, device=dev), offs.view(-1, 1, 1))
+        cs, ci, offs = self._cand
+        for s, ix in enumerate(self.shards):
+            ix.search_device(queries, k, cs[s], ci[s])
+        gi = torch.where(ci >= 0, ci + offs, ci)
+        merge_topk_device(cs, gi, k, out_scores, out_ids)
+        return out_scores, out_ids
 
 
 class ShardedSearcher:
@@ -55,8 +129,9 @@ class ShardedSearcher:
         """Global top-k of `queries` (identical on every rank) over all shards; with
         keep=(start, stop) only those query rows are merged and returned."""
         s, i = self.local_search(queries, k)
-        i = torch.where(i >= 0, i + self.offset, i)
-        gs, gi = self._all_gather(s), self._all_gather(i)  # [world, nq, k]
+        if self.offset:
+            i = torch.where(i >= 0, i + self.offset, i)
+        gs, gi = unpack_candidates(self._all_gather(pack_candidates(s, i)))  # [world, nq, k]
         if keep is not None:
             gs, gi = gs[:, keep[0]:keep[1]].contiguous(), gi[:, keep[0]:keep[1]].contiguous()
         nq = gs.shape[1]

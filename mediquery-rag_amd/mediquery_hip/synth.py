@@ -62,6 +62,13 @@ def corpus_device(n, dim, device, seed=CORPUS_SEED):
     return torch.randn((n, dim), generator=g, device=device, dtype=torch.float32)
 
 
+def corpus_shard_device(rows_per_shard, shard, dim, device, seed=CORPUS_SEED):
+    """Shard `shard` of a corpus made of equal seeded blocks (BASELINE config 4: 10M rows
+    as 8 x 1.25M): every rank regenerates only the blocks it owns, and the global corpus
+    is the same whatever the number of ranks."""
+    return corpus_device(rows_per_shard, dim, device, seed=seed + 1 + shard)
+
+
 def queries_device(b, rows_dev, seed=QUERY_SEED, planted_frac=0.5, noise=0.05):
     """Device twin of `queries` for corpora made by corpus_device."""
     import torch

@@ -53,7 +53,18 @@ class CharTokenizer:
 
 
 class WordPieceTokenizer:
-    """Uncased-Chinese-BERT style tokenisation over a local vocab file."""
+    """BERT WordPiece over a local vocab file, as the published tokenizer computes it
+    (`tokenizers` BertNormalizer + BertPreTokenizer + WordPiece, i.e.
+    transformers.BertTokenizer; pinned by tests/golden/wordpiece_golden.json):
+      1. clean: drop NUL, U+FFFD and category Cc/Cf/Co/Cs except \\t \\n \\r (unassigned
+         code points are kept); whitespace -> word break;
+      2. CJK ideographs (the crate's ranges) become words of their own;
+      3. lower_case: NFD, drop Mn, then each character's full lower-case mapping
+         (per character: no final-sigma context);
+      4. split on whitespace and isolate punctuation (ASCII symbols or category P*), on the
+         normalised characters;
+      5. greedy longest-match-first WordPiece ("##" continuations; [UNK] for a word with
+         no match or over 100 code points); [CLS] body [SEP], truncated to max_length."""
 
     def __init__(self, vocab_file, max_length=512, lower_case=True, max_chars_per_word=100):
         with open(vocab_file, "r", encoding="utf-8") as f:
@@ -67,8 +78,10 @@ class WordPieceTokenizer:
 
     @staticmethod
     def _is_cjk(cp):
+        # the tokenizers crate's table (its fourth extension range starts at 0x2B920)
         return (0x4E00 <= cp <= 0x9FFF or 0x3400 <= cp <= 0x4DBF or 0x20000 <= cp <= 0x2A6DF
-                or 0x2A700 <= cp <= 0x2CEAF or 0xF900 <= cp <= 0xFAFF or 0x2F800 <= cp <= 0x2FA1F)
+                or 0x2A700 <= cp <= 0x2B73F or 0x2B740 <= cp <= 0x2B81F or 0x2B920 <= cp <= 0x2CEAF
+                or 0xF900 <= cp <= 0xFAFF or 0x2F800 <= cp <= 0x2FA1F)
 
     @staticmethod
     def _is_punct(ch):
@@ -76,6 +89,16 @@ class WordPieceTokenizer:
         if 33 <= cp <= 47 or 58 <= cp <= 64 or 91 <= cp <= 96 or 123 <= cp <= 126:
             return True
         return unicodedata.category(ch).startswith("P")
+
+    @staticmethod
+    def _is_control(ch):
+        return ch not in "\t\n\r" and unicodedata.category(ch) in ("Cc", "Cf", "Co", "Cs")
+
+    def _normalise(self, ch):
+        if not self.lower_case:
+            return ch
+        d = unicodedata.normalize("NFD", ch)
+        return "".join(c.lower() for c in d if unicodedata.category(c) != "Mn")
 
     def _basic(self, text):
         words, cur = [], []
@@ -86,22 +109,21 @@ class WordPieceTokenizer:
                 cur.clear()
         for ch in text:
             cp = ord(ch)
-            if cp == 0 or cp == 0xFFFD or unicodedata.category(ch) in ("Cc", "Cf") and ch not in "\t\n\r":
+            if cp == 0 or cp == 0xFFFD or self._is_control(ch):
                 continue
             if ch.isspace():
                 flush()
-            elif self._is_cjk(cp) or self._is_punct(ch):
+            elif self._is_cjk(cp):
                 flush()
-                words.append(ch)
+                words.append(self._normalise(ch))
             else:
-                cur.append(ch)
+                for c in self._normalise(ch):
+                    if self._is_punct(c):
+                        flush()
+                        words.append(c)
+                    else:
+                        cur.append(c)
         flush()
-        if self.lower_case:
-            out = []
-            for w in words:
-                w = unicodedata.normalize("NFD", w.lower())
-                out.append("".join(c for c in w if unicodedata.category(c) != "Mn"))
-            words = out
         return [w for w in words if w]
 
     def _wordpiece(self, word):

@@ -116,3 +116,19 @@ def test_ingest_sharded_blocks_line_up_with_search_ids(world, N, chunk):
         seen.append((off, cnt))
     assert seen[0][0] == 0 and sum(c for _, c in seen) == N
     assert all(seen[r][0] + seen[r][1] == seen[r + 1][0] for r in range(world - 1))
+
+
+def test_pack_candidates_roundtrip_is_bit_exact():
+    """The single candidate all-gather carries (score, id) as one int32 [nq, k, 3]
+    tensor: scores (incl. -inf padding, -0.0, subnormals) and ids (incl. -1 and ids past
+    2^32) must come back bit-exactly."""
+    from mediquery_hip.distributed import pack_candidates, unpack_candidates
+    s = torch.tensor([[1.0, -0.0, float("-inf")], [1e-40, 0.5, -2.5]], dtype=torch.float32)
+    i = torch.tensor([[0, 5_000_000_000, -1], [7, 2**31 + 3, 123]], dtype=torch.int64)
+    p = pack_candidates(s, i)
+    assert p.dtype == torch.int32 and p.shape == (2, 3, 3)
+    g = torch.stack([p, p])  # what an all-gather of two ranks stacks
+    s2, i2 = unpack_candidates(g)
+    assert s2.shape == (2, 2, 3) and i2.shape == (2, 2, 3)
+    assert torch.equal(s2[1].view(torch.int32), s.view(torch.int32))
+    assert torch.equal(i2[0], i)

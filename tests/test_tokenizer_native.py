@@ -45,3 +45,26 @@ def test_wordpiece_native_matches_python(golden, tmp_path):
     nat = NativeTokenizer.wordpiece(str(p), max_length=512)
     bad = [t[:30] for t in texts if nat.encode(t) != py.encode(t)]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("case", ["lower", "cased"])
+def test_wordpiece_matches_published_bert_tokenizer(golden, case):
+    """Bit-exact ids of transformers.BertTokenizer (the tokenizers crate's BertNormalizer
+    + BertPreTokenizer + WordPiece) on a local vocab: 154 docs, 32 queries, edge strings
+    (controls, private use, unassigned, NFD accents, Hangul, CJK compatibility and
+    extension ranges, final sigma, >100-char words, 512-token truncation).  Fixture made
+    by tests/golden/make_wordpiece_golden.py; reference site src/medical_engine.py:43."""
+    g = json.load(open(os.path.join(golden, "wordpiece_golden.json"), encoding="utf-8"))
+    c = g["cases"][case]
+    vocab = os.path.join(golden, g["vocab"])
+    nat = NativeTokenizer.wordpiece(vocab, max_length=g["max_length"], lower_case=c["do_lower_case"])
+    py = WordPieceTokenizer(vocab, max_length=g["max_length"], lower_case=c["do_lower_case"])
+    bad_n = [j for j, (t, ids) in enumerate(zip(g["texts"], c["ids"])) if nat.encode(t) != ids]
+    bad_p = [j for j, (t, ids) in enumerate(zip(g["texts"], c["ids"])) if py.encode(t) != ids]
+    assert not bad_n, [g["texts"][j][:20] for j in bad_n[:5]]
+    assert not bad_p, [g["texts"][j][:20] for j in bad_p[:5]]
+    # the batched call pads to the longest sequence, as the encoder consumes it
+    ids, mask = nat(g["texts"][:40])
+    for j in range(40):
+        n = int(mask[j].sum())
+        assert ids[j, :n].tolist() == c["ids"][j] and not ids[j, n:].any()
