@@ -426,6 +426,26 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
 #pragma unroll
   for (int j = 0; j < CH; ++j)
     wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+  // Everything else this launch reads from memory goes out now too, under the weight
+  // loads: the epilogue's bias / residual element (thread t < 256 finishes output element
+  // t of the tile) and the LayerNorm's gamma / beta.  Loaded where they are used, each
+  // would add a dependent memory round trip to the launch's critical path (after the
+  // partial-tile reduction, after the row statistics).
+  const int et = threadIdx.x;
+  const int erow = r0 + et / kRT, ecol = n0 + et % kRT;
+  float ebias = 0.f, eres = 0.f;
+  if (et < kRT * kRT && ks == 0 && erow < M) {
+    ebias = bias[ecol];
+    if (EPI == EPI_RESID) eres = resid[(int64_t)erow * ldr + ecol];
+  }
+  floatx4 lgv[LN_IN ? VPL : 1], lbv[LN_IN ? VPL : 1];
+  if (LN_IN) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      lgv[i] = *reinterpret_cast<const floatx4*>(lng + (i * 64 + lane) * 4);
+      lbv[i] = *reinterpret_cast<const floatx4*>(lnb + (i * 64 + lane) * 4);
+    }
+  }
   if (LN_IN) {
     const int row = r0 + wave;  // one wave per row (kRWaves == kRT)
     const float* src = A + (int64_t)min(row, M - 1) * lda;
@@ -465,8 +485,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int cc = (i * 64 + lane) * 4;
-      x[i] = (x[i] - mu) * rs * *reinterpret_cast<const floatx4*>(lng + cc) +
-             *reinterpret_cast<const floatx4*>(lnb + cc);
+      x[i] = (x[i] - mu) * rs * lgv[i] + lbv[i];
       *reinterpret_cast<floatx4*>(&arows[wave * AS + cc]) = x[i];
     }
     // LDS-only barrier: the weight loads stay in flight across it
@@ -512,20 +531,18 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) part[wave][(4 * kq + j) * kRT + c] = acc[j];
   __syncthreads();
-  if (threadIdx.x >= kRT * kRT) return;
-  const int rr = threadIdx.x / kRT, cc = threadIdx.x % kRT;
-  const int row = r0 + rr, col = n0 + cc;
-  float v = part[0][threadIdx.x];
+  if (et >= kRT * kRT) return;
+  float v = part[0][et];
 #pragma unroll
-  for (int w = 1; w < kRWaves; ++w) v += part[w][threadIdx.x];
-  if (row >= M) return;
+  for (int w = 1; w < kRWaves; ++w) v += part[w][et];
+  if (erow >= M) return;
   if (ks == 0) {  // split 0 carries bias / residual; GELU needs an unsplit K
-    v += bias[col];
+    v += ebias;
     if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
     if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
-    if (EPI == EPI_RESID) v += resid[(int64_t)row * ldr + col];
+    if (EPI == EPI_RESID) v += eres;
   }
-  out[ks * o_plane + (int64_t)row * ldo + col] = v;
+  out[ks * o_plane + (int64_t)erow * ldo + ecol] = v;
 }
 
 // One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).

@@ -849,8 +849,11 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
   }
   // Per wave: Tw = the largest key with at least k_out of the WAVE's heads >= Tw (bitwise
   // search, ballot counts, no block barrier); T = max over the 4 waves still has k_out
-  // heads >= T (all in one wave), so it is a valid threshold - at most ~4x more
-  // survivors than the block-wide k_out-th head, for 62 fewer barriers.
+  // heads >= T (all in one wave), so it is a valid threshold, for 62 fewer barriers.
+  // Survivors are usually a few times the block-wide k_out-th head's, but nothing bounds
+  // them: when no single wave holds k_out valid heads (many empty lists) T = 0 and every
+  // valid entry is admitted; past kSelCap the block falls back to the thread-list merge
+  // below, so results stay exact either way.
   const int jn = min(kSelHeads, (n_lists + 255) / 256);  // head slots in use
   unsigned T = 0;
   for (int b = 31; b >= 0; --b) {
@@ -986,10 +989,12 @@ struct mq_index {
   int* host_flag = nullptr;  // pinned: the status word a search reads back (a pageable
                              // 4-byte D2H copy is staged and costs more than the scan tail)
   DevBuf stage, cand_s, cand_i, out_s, out_i;
+  DevBuf sel;  // device copy of a mq_index_select row list
   DevBuf rows16;     // bf16 shadow of `rows` for the coarse path ([cap, dim] bf16)
   int64_t n16 = 0;   // rows already mirrored into rows16
   DevBuf stats16;    // shadow rounding maxima: [0] max ||c - bf16(c)||, [1] max ||c|| (float bits)
   DevBuf q16, coarse_s, coarse_i;
+  DevBuf fb_cs, fb_ci;  // coarse candidates of the bf16-mode queries re-run on the tiled scan
   DevBuf flag;          // merge overflow flag (k > 16) / screen failure count
   DevBuf tier_fail[4], tier_q[4], tier_s[4], tier_i[4];  // per screen tier: re-run subset
   int64_t rescans = 0;   // searches re-run with 64-entry scan lists
@@ -1265,7 +1270,7 @@ bool thresh_ok(const mq_index* ix, int64_t nq) {
 }
 
 int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
-                hipStream_t s) {
+                hipStream_t s, int tau_rank, int* fail_count, int64_t* fail) {
   const size_t n_lists = 2 * (size_t)ix->num_cus;
   int rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
   if (!rc) rc = ix->ts_tau.ensure(nq * sizeof(float));
@@ -1275,7 +1280,7 @@ int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, i
   if (rc) return rc;
   ThreshArgs a{q16, (int)nq, ix->rows16.as<unsigned char>(), ix->n, ix->dim, ix->num_cus, kc,
                ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
-               ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi};
+               ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi, tau_rank, fail_count, fail};
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh(a, s, &ix->tl);
   ix->tl.close(s);
@@ -1337,28 +1342,75 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   return MQ_OK;
 }
 
-// the bf16 candidate scan of a batch: K9t when it applies, else the tiled K9 + K10
+// screen tiers (see search_screened)
+enum ScreenTier { TIER_BF16_STREAM = 0, TIER_BF16 = 1, TIER_X6 = 2, TIER_I8 = 3 };
+
+// the bf16 candidate scan of a batch: K9t when it applies, else the tiled K9 + K10.
+// K9t's tau is the tau_rank-th sample list maximum (the screens keep kTsRank: ~128
+// survivors, the certificate covers a short list); with `fail` set, queries whose
+// survivors overflowed kTsCap or fell short of kc are listed there for a re-run.
 int bf16_candidates(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
-                    hipStream_t s) {
-  if (thresh_ok(ix, nq)) return thresh_topk(ix, q16, nq, kc, os, oi, s);
+                    hipStream_t s, int tau_rank = kTsRank, int* fail_count = nullptr,
+                    int64_t* fail = nullptr) {
+  if (thresh_ok(ix, nq)) return thresh_topk(ix, q16, nq, kc, os, oi, s, tau_rank, fail_count, fail);
   return scan_topk(ix, SCAN_BF16, q16, nq, kc, os, oi, s);
 }
 
 // Config 5: bf16 coarse scan for the best `kc` rows per query (kc = max(2k, 50) capped
 // at MQ_MAX_K and n), then an exact fp32 re-rank of those candidates to the final top-k.
+// No certificate covers this mode, so every query must come out of the threshold scan
+// with at least kc survivors: tau sits at the min(kc, 24)-th sample list maximum (at
+// least that many survivors by construction; ~24 x 16 = 384 expected at the 1/16 sample,
+// so fewer than 64 is a > 4-sigma event - tau at the 64th would keep ~1024 and cost the
+// scan ~50%), and a query whose survivors still fall short of kc, or overflow kTsCap
+// (heavy duplicates), is re-run on the tiled bf16 scan, which always yields the exact
+// bf16 top-kc.  Synchronous when the threshold scan ran.
 int search_bf16_rerank(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                        hipStream_t s) {
   int rc = ensure_shadow(ix, s);
   if (!rc) rc = queries_to_bf16(ix, q, nq, s);
   if (rc) return rc;
   const int kc = (int)std::min<int64_t>(std::max(2 * k, 50), std::min<int64_t>(MQ_MAX_K, ix->n));
+  const bool ts = thresh_ok(ix, nq);
   rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
   if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
-  if (!rc) rc = bf16_candidates(ix, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(),
-                                ix->coarse_i.as<int64_t>(), s);
+  if (!rc && ts) rc = ix->flag.ensure(sizeof(int));
+  if (!rc && ts) rc = ix->tier_fail[TIER_BF16].ensure((size_t)nq * sizeof(int64_t));
+  if (rc) return rc;
+  int64_t* fail = ts ? ix->tier_fail[TIER_BF16].as<int64_t>() : nullptr;
+  if (ts) MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
+  rc = bf16_candidates(ix, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(),
+                       s, std::min(kc, 24), ts ? ix->flag.as<int>() : nullptr, fail);
   if (rc) return rc;
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
                      ix->coarse_i.as<int64_t>(), kc, k, os, oi, nullptr, kNoPrune, nullptr);
+  MQ_HIP(hipGetLastError());
+  if (!ts) return MQ_OK;
+  int n_fail = 0;
+  rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);
+  if (rc || n_fail == 0) return rc;
+  ++ix->rescans;
+  rc = ix->tier_q[TIER_BF16].ensure((size_t)n_fail * ix->dim * sizeof(float));
+  if (!rc) rc = ix->tier_s[TIER_BF16].ensure((size_t)n_fail * k * sizeof(float));
+  if (!rc) rc = ix->tier_i[TIER_BF16].ensure((size_t)n_fail * k * sizeof(int64_t));
+  if (!rc) rc = ix->fb_cs.ensure((size_t)n_fail * kc * sizeof(float));
+  if (!rc) rc = ix->fb_ci.ensure((size_t)n_fail * kc * sizeof(int64_t));
+  if (rc) return rc;
+  float* sq = ix->tier_q[TIER_BF16].as<float>();
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n_fail + 3) / 4)), dim3(256), 0, s, q, fail,
+                     (int64_t)n_fail, ix->dim, sq);
+  MQ_HIP(hipGetLastError());
+  rc = queries_to_bf16(ix, sq, n_fail, s);
+  if (!rc) rc = scan_topk(ix, SCAN_BF16, ix->q16.as<float>(), n_fail, kc, ix->fb_cs.as<float>(),
+                          ix->fb_ci.as<int64_t>(), s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)n_fail), dim3(256), 0, s, sq, ix->rows, ix->dim,
+                     ix->fb_ci.as<int64_t>(), kc, k, ix->tier_s[TIER_BF16].as<float>(),
+                     ix->tier_i[TIER_BF16].as<int64_t>(), nullptr, kNoPrune, nullptr);
+  const int64_t total = (int64_t)n_fail * k;
+  hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     ix->tier_s[TIER_BF16].as<float>(), ix->tier_i[TIER_BF16].as<int64_t>(), fail,
+                     (int64_t)n_fail, k, os, oi);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1385,7 +1437,6 @@ int search_direct(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
 //   TIER_I8           one query: int8 shadow threshold scan (K9q, a quarter of the fp32
 //                     bytes) for 64 candidates -> TIER_BF16_STREAM
 // Synchronous (reads the failure count).
-enum ScreenTier { TIER_BF16_STREAM = 0, TIER_BF16 = 1, TIER_X6 = 2, TIER_I8 = 3 };
 
 bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
   return nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024;
@@ -1671,31 +1722,32 @@ int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst
     MQ_CHECK_ARG(rows[i] >= 0 && rows[i] < src->n, "row %lld out of range (n=%lld)",
                  (long long)rows[i], (long long)src->n);
   DeviceGuard dg(src->device);
+  // gather straight into dst's slab when it is a different index with room (a reused
+  // scratch index for filtered searches: no allocation); else into a fresh slab
+  const bool in_place_slab = src != dst && dst->rows && dst->cap >= n;
   float* fresh = nullptr;
-  int64_t* sel = nullptr;
   if (n > 0) {
-    if (hipMalloc((void**)&fresh, (size_t)n * src->dim * sizeof(float)) != hipSuccess)
+    int rc = src->sel.ensure((size_t)n * sizeof(int64_t));
+    if (rc) return rc;
+    if (!in_place_slab && hipMalloc((void**)&fresh, (size_t)n * src->dim * sizeof(float)) != hipSuccess)
       MQ_FAIL(MQ_ENOMEM, "hipMalloc of %lld rows failed", (long long)n);
-    if (hipMalloc((void**)&sel, (size_t)n * sizeof(int64_t)) != hipSuccess) {
-      (void)hipFree(fresh);
-      MQ_FAIL(MQ_ENOMEM, "hipMalloc of the row list failed");
-    }
-    hipError_t e = hipMemcpy(sel, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpy(src->sel.p, rows, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, nullptr,
-                         src->rows, sel, n, src->dim, fresh);
+                         src->rows, src->sel.as<int64_t>(), n, src->dim, in_place_slab ? dst->rows : fresh);
       e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    (void)hipFree(sel);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess) {
-      (void)hipFree(fresh);
+      if (fresh) (void)hipFree(fresh);
       MQ_FAIL(MQ_EHIP, "row gather failed: %s", hipGetErrorString(e));
     }
   }
-  if (dst->rows) MQ_HIP(hipFree(dst->rows));
-  dst->rows = fresh;
-  dst->cap = n;
+  if (!in_place_slab) {
+    if (dst->rows) MQ_HIP(hipFree(dst->rows));
+    dst->rows = fresh;
+    dst->cap = n;
+  }
   dst->n = n;
   dst->n16 = 0;
   dst->n8 = 0;

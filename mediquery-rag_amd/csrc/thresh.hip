@@ -38,7 +38,6 @@ constexpr int kTsWaves = 8;      // waves per workgroup (32 queries each)
 constexpr int kTsQ = kTsWaves * 32;  // queries per workgroup
 constexpr int kTsBufs = 3;       // LDS ring depth
 constexpr int kTsPeriod = 16;    // sample pass: every 16th block
-constexpr int kTsRank = 8;       // tau = 8th largest list maximum of the sample (~128 survivors)
 
 enum { TS_MAX = 0, TS_APPEND = 1 };
 
@@ -230,8 +229,10 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
 // lists saw a row), and the survivor count reset.  One wave per query.  The kTsRank-th
 // largest list maximum is <= the kTsRank-th best sampled score (each of the top lists
 // holds a distinct sampled row), so at least kTsRank rows survive.
+// rank <= 64: each lane keeps its best kTsRank lists (all of them when n_lists <= 512 =
+// 2 x 256 CUs; with more, dropping a lane's lower maxima can only lower tau).
 __global__ __launch_bounds__(256) void bf16_tau_kernel(const float* __restrict__ lmax, int n_lists,
-                                                       int nq, float* __restrict__ tau,
+                                                       int nq, int rank, float* __restrict__ tau,
                                                        int* __restrict__ count) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(256) void bf16_tau_kernel(const float* __restrict__
     if (t.beats_tail(x, l)) t.insert(x, l);
   }
   float kth = -INFINITY;
-  for (int r = 0; r < kTsRank; ++r) {
+  for (int r = 0; r < rank; ++r) {
     float bs = t.s[0];
     int bi = t.id[0], bt = lane;
 #pragma unroll
@@ -269,18 +270,23 @@ __global__ __launch_bounds__(256) void bf16_tau_kernel(const float* __restrict__
 // query; slots past the survivor count hold (tau, -1), so the certificate's bound on a
 // non-candidate is max(kc-th survivor, tau).  More than kTsCap survivors: the kept set
 // is incomplete and the bound is set to +inf (the certificate then fails, the query is
-// re-run one tier down).
+// re-run one tier down).  With `fail` set (the approximate bf16 mode, no certificate), a
+// query with more than kTsCap or fewer than kc survivors is appended to fail[] instead,
+// for the caller to re-run on the tiled scan.
 __global__ __launch_bounds__(256) void bf16_select_kernel(const float* __restrict__ cs,
                                                           const int* __restrict__ ci,
                                                           const int* __restrict__ count,
                                                           const float* __restrict__ tau, int kc,
                                                           float* __restrict__ out_s,
-                                                          int64_t* __restrict__ out_i) {
+                                                          int64_t* __restrict__ out_i,
+                                                          int* __restrict__ fail_count,
+                                                          int64_t* __restrict__ fail) {
   __shared__ float ls[kTsCap];
   __shared__ int li[kTsCap];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
   const int total = count[q];
+  if (fail && tid == 0 && (total > kTsCap || total < kc)) fail[atomicAdd(fail_count, 1)] = q;
   const int cnt = min(total, kTsCap);
   for (int i = tid; i < cnt; i += 256) {
     ls[i] = cs[q * kTsCap + i];
@@ -317,14 +323,14 @@ void launch_nch(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_MAX>), dim3(G, gy), dim3(512), 0, s, qb, a.nq, a.rows,
                      a.n, n_blocks, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci);
   tl->mark(s, 1);
-  hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, 2 * G, a.nq, a.tau,
-                     a.count);
+  hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, 2 * G, a.nq,
+                     a.tau_rank, a.tau, a.count);
   tl->mark(s, 0);
   hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_APPEND>), dim3(G, gy), dim3(512), 0, s, qb, a.nq,
                      a.rows, a.n, n_blocks, 1, a.tau, a.lmax, a.count, a.cs, a.ci);
   tl->mark(s, 1);
   hipLaunchKernelGGL(bf16_select_kernel, dim3(a.nq), dim3(256), 0, s, a.cs, a.ci, a.count, a.tau, a.kc,
-                     a.out_s, a.out_i);
+                     a.out_s, a.out_i, a.fail_count, a.fail);
 }
 
 void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
@@ -640,7 +646,8 @@ void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
 
 void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,
                    float* out_s, int64_t* out_i, hipStream_t s) {
-  hipLaunchKernelGGL(bf16_select_kernel, dim3(nq), dim3(256), 0, s, cs, ci, count, tau, kc, out_s, out_i);
+  hipLaunchKernelGGL(bf16_select_kernel, dim3(nq), dim3(256), 0, s, cs, ci, count, tau, kc, out_s, out_i,
+                     nullptr, nullptr);
 }
 
 // one query per launch (the single-query latency path; NQ > 1 costs registers: 256 VGPRs

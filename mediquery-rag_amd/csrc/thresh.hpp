@@ -9,6 +9,7 @@ namespace mq {
 constexpr int kTsRows = 32;          // rows per streamed block (the MFMA tile edge)
 constexpr int kTsCap = 4096;         // survivors kept per query
 constexpr int64_t kTsMinRows = 65536;  // below this the tiled K9 + K10 path is used
+constexpr int kTsRank = 8;  // screens: tau = 8th largest sample list maximum (~128 survivors)
 
 struct ThreshArgs {
   const float* q16;           // bf16 queries [nq][dim] (as packed pairs)
@@ -25,6 +26,9 @@ struct ThreshArgs {
   int* ci;                    // [nq][kTsCap] survivor rows
   float* out_s;               // [nq][kc] candidates, (score desc, id asc)
   int64_t* out_i;
+  int tau_rank;               // tau = the tau_rank-th largest sample list maximum (>= tau_rank survivors)
+  int* fail_count;            // optional: queries with more than kTsCap or fewer than kc survivors
+  int64_t* fail;              //   are appended to fail[] (count in *fail_count, zeroed by the caller)
 };
 
 // Enqueue the four K9t launches on `s`; timeline stage 0 = the two scans, 1 = tau + select.

@@ -66,6 +66,96 @@ def _match(meta, where):
     return True
 
 
+_MISSING = object()
+
+
+def _pred(op, v, x):
+    """One Chroma where-operator on one metadata value (v None = key absent), as _match."""
+    if op == "$eq":
+        return v == x
+    if op == "$ne":
+        return v != x
+    if op in ("$gt", "$gte", "$lt", "$lte"):
+        if v is None:
+            return False
+        return {"$gt": lambda: v > x, "$gte": lambda: v >= x, "$lt": lambda: v < x,
+                "$lte": lambda: v <= x}[op]()
+    if op == "$in":
+        return v in x
+    if op == "$nin":
+        return v not in x
+    raise ValueError("unsupported filter operator %r" % op)
+
+
+class _MetaColumns:
+    """Metadata held column-wise for vectorised Chroma `where` filters: per key, int32
+    codes [n] (-1 = key absent in that row) into the key's distinct values.  A condition
+    is evaluated once per DISTINCT value (Python) and mapped onto the rows by numpy, so a
+    filter over 1M rows costs milliseconds; results equal `_match` row by row."""
+
+    def __init__(self):
+        self.n = 0
+        self.cols = {}  # key -> [codes np.int32 (capacity >= n), values list, {hash key: code}]
+
+    @staticmethod
+    def _hkey(v):
+        try:
+            return (type(v).__name__, v, hash(v))
+        except TypeError:  # unhashable (list) values: keyed by their repr
+            return (type(v).__name__, repr(v), None)
+
+    def append(self, metas):
+        m = len(metas)
+        need = self.n + m
+        for col in self.cols.values():
+            if col[0].shape[0] < need:
+                grown = np.full(max(need, 2 * col[0].shape[0]), -1, np.int32)
+                grown[:self.n] = col[0][:self.n]
+                col[0] = grown
+            col[0][self.n:need] = -1
+        for r, meta in enumerate(metas):
+            for key, v in meta.items():
+                col = self.cols.get(key)
+                if col is None:
+                    col = self.cols[key] = [np.full(max(need, 1024), -1, np.int32), [], {}]
+                hk = self._hkey(v)
+                code = col[2].get(hk)
+                if code is None:
+                    code = col[2][hk] = len(col[1])
+                    col[1].append(v)
+                col[0][self.n + r] = code
+        self.n = need
+
+    def compact(self, keep):
+        """Keep rows `keep` (sorted int64 row ids), in order."""
+        for col in self.cols.values():
+            col[0] = np.ascontiguousarray(col[0][:self.n][keep])
+        self.n = len(keep)
+
+    def mask(self, where):
+        out = np.ones(self.n, bool)
+        for key, cond in where.items():
+            if key == "$and":
+                for c in cond:
+                    out &= self.mask(c)
+            elif key == "$or":
+                any_ = np.zeros(self.n, bool)
+                for c in cond:
+                    any_ |= self.mask(c)
+                out &= any_
+            else:
+                col = self.cols.get(key)
+                codes = col[0][:self.n] if col is not None else np.full(self.n, -1, np.int32)
+                values = col[1] if col is not None else []
+                ops = cond.items() if isinstance(cond, dict) else (("$eq", cond),)
+                for op, x in ops:
+                    pick = [c for c, v in enumerate(values) if _pred(op, v, x)]
+                    if _pred(op, None, x):
+                        pick.append(-1)
+                    out &= np.isin(codes, np.asarray(pick, np.int32)) if pick else False
+        return out
+
+
 def _check_k(k, n_candidates):
     """Result count of a top-k over n_candidates rows; raises past the device limit."""
     kk = min(int(k), int(n_candidates))
@@ -92,6 +182,11 @@ class HipChroma(VectorStoreBase):
         self._device = device
         self._auto_persist = bool(auto_persist)
         self._ids, self._texts, self._metas = [], [], []
+        self._id_row = {}              # id -> row (upsert / delete / get by id in O(1))
+        self._cols = _MetaColumns()    # metadata column-wise, for vectorised filters
+        self._version = 0              # bumped by every write (filtered-search cache key)
+        self._scratch = None           # reused device index for filtered searches
+        self._scratch_key = None       # (filter, version) whose rows the scratch holds
         self._index = None
         self._dim = dim
         self._slab_name = None
@@ -143,10 +238,27 @@ class HipChroma(VectorStoreBase):
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, side)  # the commit point
-        old, self._slab_name = self._slab_name, slab
-        for stale in (old, self._FILES[0] % self._collection_name):
-            if stale and stale != slab and os.path.exists(os.path.join(d, stale)):
-                os.remove(os.path.join(d, stale))
+        self._slab_name = slab
+        self._remove_orphan_slabs()
+
+    def _remove_orphan_slabs(self):
+        """Delete slabs of this collection the committed sidecar does not name: the one a
+        previous persist replaced, and any a crash or a concurrent writer left behind
+        between its slab write and its commit (each is a full copy of the index)."""
+        d = self._persist_directory
+        prefix = "mq_%s." % self._collection_name
+        for f in os.listdir(d):
+            if f.startswith(prefix) and f.endswith(".flat") and f != self._slab_name:
+                try:
+                    os.remove(os.path.join(d, f))
+                except OSError:
+                    pass
+
+    def _reindex_host(self):
+        self._id_row = {i: r for r, i in enumerate(self._ids)}
+        self._cols = _MetaColumns()
+        self._cols.append(self._metas)
+        self._version += 1
 
     def _load(self):
         with open(self._path(1), "r", encoding="utf-8") as f:
@@ -159,6 +271,9 @@ class HipChroma(VectorStoreBase):
         if len(self._index) != len(self._ids):
             raise RuntimeError("persisted index (%d rows) and sidecar (%d ids) disagree"
                                % (len(self._index), len(self._ids)))
+        self._reindex_host()
+        if os.access(self._persist_directory, os.W_OK):
+            self._remove_orphan_slabs()
 
     def _embed_query(self, query):
         if self._embedding_function is None:
@@ -193,36 +308,55 @@ class HipChroma(VectorStoreBase):
         """Upsert semantics as in Chroma: an existing id is replaced (row rebuilt)."""
         emb = np.ascontiguousarray(embeddings, dtype=np.float32)
         self._ensure_index(emb.shape[1])
-        existing = set(self._ids).intersection(ids)
+        if len(set(ids)) != len(ids):  # last write of a repeated id wins, as in an upsert
+            last = {i: j for j, i in enumerate(ids)}
+            pick = sorted(last.values())
+            emb, texts = emb[pick], [texts[j] for j in pick]
+            metadatas, ids = [metadatas[j] for j in pick], [ids[j] for j in pick]
+        existing = [i for i in ids if i in self._id_row]
         if existing:
-            self.delete(list(existing), _persist=False)
+            self.delete(existing, _persist=False)
         self._index.add(emb)
+        base = len(self._ids)
         self._ids += ids
         self._texts += texts
         self._metas += metadatas
+        self._id_row.update((i, base + j) for j, i in enumerate(ids))
+        self._cols.append(metadatas)
+        self._version += 1
         self._persist()
 
     def delete(self, ids=None, _persist=True, **kwargs):
         if not ids or self._index is None:
             return None
-        drop = set(ids)
-        keep = [r for r, i in enumerate(self._ids) if i not in drop]
+        drop = [self._id_row[i] for i in set(ids) if i in self._id_row]
+        if not drop:
+            return True
+        keepm = np.ones(len(self._ids), bool)
+        keepm[drop] = False
+        keep = np.flatnonzero(keepm)
         self._index.select(keep, out=self._index)  # device compaction, rows bit-identical
-        self._ids = [self._ids[r] for r in keep]
-        self._texts = [self._texts[r] for r in keep]
-        self._metas = [self._metas[r] for r in keep]
+        n = len(self._ids)
+        for name in ("_ids", "_texts", "_metas"):
+            arr = np.empty(n, object)
+            for r, v in enumerate(getattr(self, name)):  # (dicts must not be unpacked)
+                arr[r] = v
+            setattr(self, name, arr[keep].tolist())
+        self._cols.compact(keep)
+        self._id_row = {i: r for r, i in enumerate(self._ids)}
+        self._version += 1
         if _persist:
             self._persist()
         return True
 
     def get(self, ids=None, where=None, limit=None, offset=None, include=None, **kwargs):
-        rows = range(len(self._ids))
+        rows = np.arange(len(self._ids))
         if ids is not None:
-            want = set([ids] if isinstance(ids, str) else ids)
-            rows = [r for r in rows if self._ids[r] in want]
+            want = [ids] if isinstance(ids, str) else ids
+            rows = np.array(sorted({self._id_row[i] for i in want if i in self._id_row}), np.int64)
         if where:
-            rows = [r for r in rows if _match(self._metas[r], where)]
-        rows = list(rows)[offset or 0:]
+            rows = rows[self._cols.mask(where)[rows]]
+        rows = rows.tolist()[offset or 0:]
         if limit is not None:
             rows = rows[:limit]
         return {"ids": [self._ids[r] for r in rows], "documents": [self._texts[r] for r in rows],
@@ -239,15 +373,21 @@ class HipChroma(VectorStoreBase):
             kk = _check_k(k, n)
             s, i = self._index.search(q, kk)
             return [(int(r), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
-        allowed = np.array([r for r in range(n) if _match(self._metas[r], filter)], dtype=np.int64)
+        # exact filtered search: score only the allowed rows, gathered on the device into
+        # one reused scratch index (rows bit-identical to the store's); a repeated filter
+        # on an unchanged store reuses the gathered rows
+        key = (json.dumps(filter, sort_keys=True, default=repr), self._version)
+        if key != self._scratch_key:
+            allowed = np.flatnonzero(self._cols.mask(filter)).astype(np.int64)
+            if self._scratch is None:
+                self._scratch = FlatIndex(dim=self._dim, device=self._device)
+            self._index.select(allowed, out=self._scratch)
+            self._scratch_rows, self._scratch_key = allowed, key
+        allowed = self._scratch_rows
         if len(allowed) == 0:
             return []
-        # exact filtered search: score only the allowed rows, gathered on the device into
-        # a scratch index (rows bit-identical to the store's)
-        sub = self._index.select(allowed)
         kk = _check_k(k, len(allowed))
-        s, i = sub.search(q, kk)
-        sub.close()
+        s, i = self._scratch.search(q, kk)
         return [(int(allowed[r]), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
 
     def similarity_search_by_vector_with_score(self, embedding, k=DEFAULT_K, filter=None, **kwargs):

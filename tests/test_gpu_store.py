@@ -114,3 +114,58 @@ def test_k_limit_and_crash_safe_persist(embeddings, docs, tmp_path):
         HipChroma(persist_directory=str(old), embedding_function=embeddings)
     HipChroma.from_documents(documents=docs[:5], embedding=embeddings, persist_directory=str(old))
     assert len(HipChroma(persist_directory=str(old), embedding_function=embeddings)) == 5
+
+
+def test_upsert_by_existing_id_replaces_row_and_persists(embeddings, docs, tmp_path):
+    """Chroma upsert semantics (`add_texts` with an id that exists, reference ingest
+    src/ingest_medical.py:106-110 runs through add_texts): the row is replaced - one row
+    per id, searches return the new text and metadata, a persisted reload agrees, and
+    orphaned slabs (a crash between slab write and commit) are cleaned up on load."""
+    db = str(tmp_path / "db")
+    ids = ["doc%03d" % i for i in range(30)]
+    store = HipChroma.from_documents(documents=docs[:30], embedding=embeddings, ids=ids,
+                                     persist_directory=db)
+    new_text = "更新后的内容：每天步行八千步有益健康"
+    store.add_texts([new_text, docs[40].page_content], metadatas=[{"title": "updated"}, {"title": "d40"}],
+                    ids=["doc007", "doc100"])
+    assert len(store) == 31
+    got = store.get(ids=["doc007"])
+    assert got["documents"] == [new_text] and got["metadatas"] == [{"title": "updated"}]
+    top = store.similarity_search(new_text, k=1)[0]
+    assert top.page_content == new_text and top.metadata["title"] == "updated"
+    assert all(d.page_content != docs[7].page_content for d in store.similarity_search(docs[7].page_content, k=5))
+    # repeated ids inside one call: the last one wins
+    store.add_texts(["甲", "乙"], ids=["dupe", "dupe"])
+    assert store.get(ids=["dupe"])["documents"] == ["乙"] and len(store) == 32
+    # filtered search after writes sees the new rows (the filter cache is keyed on writes)
+    assert [d.page_content for d in store.similarity_search(new_text, k=3, filter={"title": "updated"})] == [new_text]
+    store.delete(["doc007"])
+    assert store.similarity_search(new_text, k=3, filter={"title": "updated"}) == []
+    open(os.path.join(db, "mq_langchain.deadbeef0000.flat"), "wb").write(b"orphan")
+    again = HipChroma(persist_directory=db, embedding_function=embeddings)
+    assert len(again) == 31 and again.get(ids=["doc007"])["ids"] == []
+    assert again.get(ids=["dupe"])["documents"] == ["乙"]
+    assert [f for f in os.listdir(db) if f.endswith(".flat")] == [again._slab_name]
+    s1 = [d.page_content for d in store.similarity_search(docs[3].page_content, k=5)]
+    s2 = [d.page_content for d in again.similarity_search(docs[3].page_content, k=5)]
+    assert s1 == s2
+
+
+def test_filtered_search_equals_oracle_on_allowed_rows(embeddings, docs):
+    """filter= scores only the allowed rows (vectorised where, device gather into one
+    reused scratch index): the result equals the exact top-k over the rows _match admits,
+    for several filters in a row and for a repeated one."""
+    from mediquery_hip.vectorstore import _match
+    store = HipChroma.from_documents(documents=docs, embedding=embeddings)
+    emb = embeddings.embed_array([d.page_content for d in docs])
+    titles = sorted({d.metadata["title"] for d in docs})
+    filters = [{"source": "《超越百岁》"}, {"title": {"$in": titles[:40]}},
+               {"$or": [{"title": titles[3]}, {"title": titles[9]}]}, {"title": {"$in": titles[:40]}}]
+    q = docs[11].page_content
+    qe = embeddings.embed_array([q])
+    for f in filters:
+        allowed = np.array([r for r, d in enumerate(docs) if _match(d.metadata, f)])
+        got = store._search_rows(qe[0], 5, f)
+        ref = exact_scores(qe, emb[allowed])[0]
+        order = np.lexsort((allowed, -ref))[:5]
+        assert [r for r, _ in got] == allowed[order].tolist(), f

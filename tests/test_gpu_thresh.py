@@ -112,3 +112,42 @@ def test_threshold_scan_full_size_planted(require_gpu):
     torch.cuda.synchronize()
     assert bool((i == i2).all())
     assert ix.screen_fallbacks == 0
+
+
+@pytest.mark.parametrize("clustered", [False, True])
+def test_bf16_mode_random_queries_k50_never_pad(require_gpu, clustered):
+    """MQ_DTYPE_BF16 has no certificate: its threshold scan keeps tau at the 24th sample
+    list maximum (~384 survivors) and re-runs any query left with fewer than kc (64) on
+    the tiled scan - random, non-planted queries at k = 50 never come back with -1 ids or
+    -inf scores (with tau at the 8th maximum ~1% of such queries fell short of 64)."""
+    c = synth.corpus(200000, 768, seed=11, clustered=clustered)
+    rng = np.random.default_rng(5)
+    q = rng.standard_normal((512, 768)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    ix = _index(c, _lib.MQ_DTYPE_BF16)
+    s, i = ix.search(q, 50)
+    assert (i >= 0).all() and np.isfinite(s).all()
+    assert all(len(set(r.tolist())) == 50 for r in i)
+    ref = exact_scores(q, c)
+    np.testing.assert_allclose(s, np.take_along_axis(ref, i, axis=1), rtol=0, atol=1e-5)
+    assert (np.diff(s, axis=1) <= 0).all()
+    exact = np.argsort(-ref, axis=1, kind="stable")[:, :50]
+    hits = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(i, exact))
+    assert hits / (512 * 50) >= 0.98
+
+
+def test_bf16_mode_survivor_overflow_reruns_on_tiled_scan(require_gpu):
+    """5000 exact duplicates of query 0's direction: more survivors than kTsCap, so the
+    threshold scan's kept set depends on arrival order; the query is listed by the select
+    and re-run on the tiled scan - deterministic ids: the 50 lowest duplicate rows."""
+    c = synth.corpus(90000, 768, seed=3, clustered=True)
+    q, _ = synth.queries(128, c, seed=3)
+    c[20000:25000] = q[0]
+    ix = _index(c, _lib.MQ_DTYPE_BF16)
+    r0 = ix.rescans
+    s, i = ix.search(q, 50)
+    assert ix.rescans >= r0 + 1  # the re-run (plus the tiled scan's own 64-list re-scan on 5000 ties)
+    assert i[0].tolist() == list(range(20000, 20050))
+    assert (i >= 0).all()
+    s2, i2 = ix.search(q, 50)  # deterministic across calls
+    np.testing.assert_array_equal(i, i2)

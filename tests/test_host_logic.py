@@ -89,3 +89,40 @@ def test_embeddings_refuse_silent_synthetic(tmp_path, monkeypatch):
         HipBertEmbeddings()
     with pytest.raises(ValueError, match="synthetic"):
         HipBertEmbeddings(synthetic=True, weights_path=str(w))
+
+
+def test_metadata_columns_equal_row_filter():
+    """The vectorised column filter (filtered searches, get(where=)) equals the row-wise
+    Chroma `where` semantics on random metadata: missing keys, mixed types, bool vs int,
+    compaction after deletes."""
+    from mediquery_hip.vectorstore import _MetaColumns
+    rng = np.random.default_rng(0)
+    titles = ["t%d" % i for i in range(7)]
+    metas = []
+    for r in range(3000):
+        m = {}
+        if rng.random() < 0.9:
+            m["title"] = titles[rng.integers(7)]
+        if rng.random() < 0.7:
+            m["n"] = int(rng.integers(0, 10))
+        if rng.random() < 0.3:
+            m["flag"] = bool(rng.integers(2))
+        if rng.random() < 0.2:
+            m["x"] = float(rng.standard_normal())
+        metas.append(m)
+    cols = _MetaColumns()
+    cols.append(metas[:1000])
+    cols.append(metas[1000:])
+    wheres = [{"title": "t3"}, {"n": {"$gte": 5}}, {"n": {"$lt": 2}, "title": {"$ne": "t1"}},
+              {"$or": [{"flag": True}, {"n": {"$in": [1, 3, 7]}}]}, {"missing": {"$nin": ["a"]}},
+              {"$and": [{"x": {"$gt": 0.5}}, {"title": {"$in": titles[:3]}}]}, {"flag": 1},
+              {"n": {"$ne": 4}}, {"missing": "z"}]
+    for w in wheres:
+        np.testing.assert_array_equal(cols.mask(w), [_match(m, w) for m in metas], err_msg=str(w))
+    keep = np.flatnonzero(rng.random(3000) < 0.6)
+    cols.compact(keep)
+    kept = [metas[r] for r in keep]
+    cols.append([{"title": "new", "n": 5}])
+    kept.append({"title": "new", "n": 5})
+    for w in wheres + [{"title": "new"}]:
+        np.testing.assert_array_equal(cols.mask(w), [_match(m, w) for m in kept], err_msg=str(w))

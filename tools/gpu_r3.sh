@@ -1,0 +1,11 @@
+#!/bin/bash
+# r3 check on one MI355X: new tests first, then the whole GPU suite, smoke, N=1 bench.
+set -o pipefail
+mkdir -p gpurun_out
+[ -n "$NEW_TESTS" ] && { timeout -k 10 400 python -u -m pytest $NEW_TESTS -x -v --timeout 200 --timeout-method thread > gpurun_out/new_tests.log 2>&1 || { echo NEW_TESTS_FAIL; tail -30 gpurun_out/new_tests.log; exit 1; }; }
+[ -n "$NEW_TESTS" ] && tail -1 gpurun_out/new_tests.log
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL; exit 1; }
+timeout -k 10 500 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAIL; tail -5 gpurun_out/bench.err; exit 1; }
+echo ALL_OK
