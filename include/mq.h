@@ -184,6 +184,26 @@ int mq_encoder_set_precision(mq_encoder* enc, int dtype);
  * faster for one query (0.628 vs 0.645 ms: the graph path stages ids / mask / out through
  * its own captured buffers); graphs help a host-bound caller. */
 int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
+/* Tuning options of the forward (explicit, per handle; results stay within the parity
+ * tolerances whatever they are set to - each non-default value has a GPU test):
+ *   MQ_ENC_OPT_ROWS_MAX          token rows (B x L) up to which the few-row forward runs
+ *                                (0..256, default 64; 0 = always the tiled path)
+ *   MQ_ENC_OPT_ROWS_SPLITS       few-row FFN-down K splits (0 = automatic, else 1..4 when
+ *                                it divides ffn / 256 into an instantiated depth)
+ *   MQ_ENC_OPT_SPLITK_MAX        deepest split-K of the tiled path's few-row GEMMs (2..64,
+ *                                default 16)
+ *   MQ_ENC_OPT_LN_ROWS_PER_WAVE  rows per wave of the batched LayerNorm kernel (1, 2, 4;
+ *                                default 4)
+ *   MQ_ENC_OPT_FUSE_ATTN_OPROJ   few-row forward: attention + output projection in one
+ *                                launch (1, default) or two (0)
+ * Setting an option drops the handle's captured graphs. */
+#define MQ_ENC_OPT_ROWS_MAX 0
+#define MQ_ENC_OPT_ROWS_SPLITS 1
+#define MQ_ENC_OPT_SPLITK_MAX 2
+#define MQ_ENC_OPT_LN_ROWS_PER_WAVE 3
+#define MQ_ENC_OPT_FUSE_ATTN_OPROJ 4
+int mq_encoder_set_option(mq_encoder* enc, int option, int value);
+int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);
 int mq_encoder_read_timing(mq_encoder* enc, float* ms, int n);
 /* Forward: ids/mask [B, L] int32 -> out [B, hidden] f32, unit-norm (K1..K7).

@@ -388,12 +388,37 @@ __device__ __forceinline__ void ln_row_stats_fast(const floatx4 (&x)[VPL], float
 #ifndef MQ_ROWS_DBG
 #define MQ_ROWS_DBG 0  // measurement builds only: 1 no weight loads, 2 no row loads, 4 no MFMA
 #endif
+#if MQ_ROWS_DBG != 0 && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_ROWS_DBG computes wrong results: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
+#endif
+// Measurement builds with -DMQ_KTRACE: thread 0 of each workgroup of the few-row kernels
+// stamps the 100 MHz wall clock at phase boundaries into mq_ktrace[workgroup][slot]
+// (read back by mq_debug_ktrace_read, tools/ktrace.py).  Compiled out otherwise.
+#if defined(MQ_KTRACE) && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_KTRACE is a measurement build option (-DMQ_MEASUREMENT_BUILD)"
+#endif
+#ifdef MQ_KTRACE
+// region 0 QKV, 1 FFN-up, 2 FFN-down / out-proj (rows_gemm_kernel by epilogue), 3 K3o
+constexpr int kTraceSlots = 8, kTraceWgs = 1024, kTraceRegions = 4;
+__device__ long long mq_ktrace[kTraceRegions * kTraceWgs * kTraceSlots];
+#define KTRACE_R(region, slot)                                                                 \
+  do {                                                                                        \
+    if (threadIdx.x == 0) {                                                                   \
+      const int wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);           \
+      if (wg_ < kTraceWgs) mq_ktrace[((region) * kTraceWgs + wg_) * kTraceSlots + (slot)] = wall_clock64(); \
+    }                                                                                         \
+  } while (0)
+#else
+#define KTRACE_R(region, slot) \
+  do {                         \
+  } while (0)
+#endif
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
 constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
 constexpr int kRowsDefault = 64;  // ... and does by default (MQ_ROWS_MAX overrides)
 
-template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT>
 __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ A, int lda, int64_t a_plane, int M, const float* __restrict__ lng,
     const float* __restrict__ lnb, float eps, float* __restrict__ ln_out,
@@ -402,39 +427,41 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const int* __restrict__ ids, int L, int vocab, const float* __restrict__ pos,
     const float* __restrict__ typ) {
   constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
-  // 16-deep blocks per load batch: all of them up to 12 (96 VGPRs of operands in flight,
-  // one memory round trip), else batches of 8
-  constexpr int CH = NB <= 12 ? NB : 8;
-  static_assert(NB % CH == 0, "NB must be <= 12 or a multiple of 8");
+  // 16-deep blocks per load batch: all of them while the operands fit the 128 VGPRs of a
+  // 1024-thread workgroup (one memory round trip), else batches
+  constexpr int CH = RT == 1 ? (NB <= 12 ? NB : 8) : (NB <= 6 ? NB : 4);
+  static_assert(NB % CH == 0, "the load batch must divide NB");
   static_assert(!LN_IN || NB == VPL, "LayerNorm input needs K == H");
-  // LN_IN: the 16 normalised rows, row stride K + 4 floats (a 16-lane ds_read_b128 group
-  // reads 16 rows at one k: 16 distinct 16-B bank groups)
+  static_assert(RT >= 1 && RT * kRT * kRT <= 1024, "one epilogue thread per output element");
+  // LN_IN: the RT x 16 normalised rows, row stride K + 4 floats (a 16-lane ds_read_b128
+  // group reads 16 rows at one k: 16 distinct 16-B bank groups)
   constexpr int AS = K + 4;
-  __shared__ __attribute__((aligned(16))) float arows[LN_IN ? kRT * AS : 4];
-  __shared__ float part[kRWaves][kRT * kRT];
+  __shared__ __attribute__((aligned(16))) float arows[LN_IN ? RT * kRT * AS : 4];
+  __shared__ float part[kRWaves][RT][kRT * kRT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 15, kq = lane >> 4;
-  const int n0 = blockIdx.x * kRT, r0 = blockIdx.y * kRT;
+  const int n0 = blockIdx.x * kRT, r0 = blockIdx.y * kRT * RT;
   const int kb0 = wave * (K / kRWaves);  // this wave's K range
   const int ks = blockIdx.z;  // K split: columns [ks K, (ks + 1) K) of A and W
   const float* wrow = W + (int64_t)(n0 + c) * ldw + ks * K + kb0 + 4 * kq;
-  const float* arow = A + (int64_t)min(r0 + c, M - 1) * lda + ks * K + kb0 + 4 * kq;
 
-  floatx4 wv[CH], av[CH];
+  KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 0);
+  floatx4 wv[CH], av[RT][CH];
   // the first batch of weights is in flight before anything else (the LayerNorm pass
-  // below waits on its own row loads only)
+  // below waits on its own row loads only).  All RT row tiles share each weight
+  // fragment: the launch streams W once.
 #pragma unroll
   for (int j = 0; j < CH; ++j)
     wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : *reinterpret_cast<const floatx4*>(wrow + 16 * j);
   // Everything else this launch reads from memory goes out now too, under the weight
-  // loads: the epilogue's bias / residual element (thread t < 256 finishes output element
-  // t of the tile) and the LayerNorm's gamma / beta.  Loaded where they are used, each
-  // would add a dependent memory round trip to the launch's critical path (after the
-  // partial-tile reduction, after the row statistics).
-  const int et = threadIdx.x;
-  const int erow = r0 + et / kRT, ecol = n0 + et % kRT;
+  // loads: the epilogue's bias / residual element (thread t < 256 RT finishes element
+  // t % 256 of row tile t / 256) and the LayerNorm's gamma / beta.  Loaded where they are
+  // used, each would add a dependent memory round trip to the launch's critical path
+  // (after the partial-tile reduction, after the row statistics).
+  const int et = threadIdx.x, ert = et / (kRT * kRT), ee = et % (kRT * kRT);
+  const int erow = r0 + ert * kRT + ee / kRT, ecol = n0 + ee % kRT;
   float ebias = 0.f, eres = 0.f;
-  if (et < kRT * kRT && ks == 0 && erow < M) {
+  if (ert < RT && ks == 0 && erow < M) {
     ebias = bias[ecol];
     if (EPI == EPI_RESID) eres = resid[(int64_t)erow * ldr + ecol];
   }
@@ -447,61 +474,72 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     }
   }
   if (LN_IN) {
-    const int row = r0 + wave;  // one wave per row (kRWaves == kRT)
-    const float* src = A + (int64_t)min(row, M - 1) * lda;
-    floatx4 x[VPL];
-    if constexpr (MQ_ROWS_DBG & 2) {
+    // wave w normalises rows r0 + w + 16 rt (one row per wave per row tile)
+    floatx4 x[RT][VPL];
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) x[i] = floatx4{0.1f * lane, 0.2f, 0.3f, 0.4f * wave};
-    } else if constexpr (S_IN == 0) {
-      // layer 0: the row is the embedding sum word[id] + pos[p] + type[0] (as
-      // embed_ln_kernel; A = the word table), normalised with the embedding LayerNorm
-      const int rr = min(row, M - 1);
-      int id = ids[rr];
-      id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    for (int rt = 0; rt < RT; ++rt) {
+      const int rr = min(r0 + rt * kRT + wave, M - 1);
+      const float* src = A + (int64_t)rr * lda;
+      if constexpr (MQ_ROWS_DBG & 2) {
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) x[rt][i] = floatx4{0.1f * lane, 0.2f, 0.3f, 0.4f * wave};
+      } else if constexpr (S_IN == 0) {
+        // layer 0: the row is the embedding sum word[id] + pos[p] + type[0] (as
+        // embed_ln_kernel; A = the word table), normalised with the embedding LayerNorm
+        int id = ids[rr];
+        id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+          const int cc = (i * 64 + lane) * 4;
+          x[rt][i] = *reinterpret_cast<const floatx4*>(A + (int64_t)id * K + cc) +
+                     *reinterpret_cast<const floatx4*>(pos + (int64_t)(rr % L) * K + cc) +
+                     *reinterpret_cast<const floatx4*>(typ + cc);
+        }
+      } else {
+        // the row is the sum of S_IN split-K planes of the producing GEMM, added in order
+        floatx4 p[S_IN][VPL];
+#pragma unroll
+        for (int z = 0; z < S_IN; ++z)
+#pragma unroll
+          for (int i = 0; i < VPL; ++i)
+            p[z][i] = *reinterpret_cast<const floatx4*>(src + z * a_plane + (i * 64 + lane) * 4);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+          x[rt][i] = p[0][i];
+#pragma unroll
+          for (int z = 1; z < S_IN; ++z) x[rt][i] += p[z][i];
+        }
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float mu, rs;
+      ln_row_stats_fast<VPL>(x[rt], eps, mu, rs);
 #pragma unroll
       for (int i = 0; i < VPL; ++i) {
         const int cc = (i * 64 + lane) * 4;
-        x[i] = *reinterpret_cast<const floatx4*>(A + (int64_t)id * K + cc) +
-               *reinterpret_cast<const floatx4*>(pos + (int64_t)(rr % L) * K + cc) +
-               *reinterpret_cast<const floatx4*>(typ + cc);
-      }
-    } else {
-      // the row is the sum of S_IN split-K planes of the producing GEMM, added in order
-      floatx4 p[S_IN][VPL];
-#pragma unroll
-      for (int z = 0; z < S_IN; ++z)
-#pragma unroll
-        for (int i = 0; i < VPL; ++i) p[z][i] = *reinterpret_cast<const floatx4*>(src + z * a_plane + (i * 64 + lane) * 4);
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        x[i] = p[0][i];
-#pragma unroll
-        for (int z = 1; z < S_IN; ++z) x[i] += p[z][i];
+        x[rt][i] = (x[rt][i] - mu) * rs * lgv[i] + lbv[i];
+        *reinterpret_cast<floatx4*>(&arows[(rt * kRT + wave) * AS + cc]) = x[rt][i];
       }
     }
-    float mu, rs;
-    ln_row_stats_fast<VPL>(x, eps, mu, rs);
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int cc = (i * 64 + lane) * 4;
-      x[i] = (x[i] - mu) * rs * lgv[i] + lbv[i];
-      *reinterpret_cast<floatx4*>(&arows[wave * AS + cc]) = x[i];
-    }
+    KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 1);
     // LDS-only barrier: the weight loads stay in flight across it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // the normalised rows out, 16 columns per workgroup of this row tile (not all of
+    KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 2);
+    // the normalised rows out, 16 columns per workgroup of this row group (not all of
     // them from one workgroup: the slowest workgroup sets the launch's duration)
-    if (ln_out && threadIdx.x < kRT * kRT) {
-      const int rr = threadIdx.x / kRT, cc = threadIdx.x % kRT;
+    if (ln_out && ert < RT) {
+      const int rr = ert * kRT + ee / kRT, cc = ee % kRT;
       if (r0 + rr < M)
         for (int c0 = blockIdx.x * kRT; c0 < K; c0 += gridDim.x * kRT)
           ln_out[(int64_t)(r0 + rr) * K + c0 + cc] = arows[rr * AS + c0 + cc];
     }
   }
 
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  floatx4 acc[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < NB; b += CH) {
     if (b > 0) {
@@ -509,32 +547,43 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
       for (int j = 0; j < CH; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * (b + j));
     }
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      if (LN_IN)
-        av[j] = *reinterpret_cast<const floatx4*>(&arows[c * AS + kb0 + 16 * (b + j) + 4 * kq]);
-      else
-        av[j] = (MQ_ROWS_DBG & 2) ? floatx4{0.1f, 0.2f, 0.3f, 0.4f}
-                                  : *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* arow = A + (int64_t)min(r0 + rt * kRT + c, M - 1) * lda + ks * K + kb0 + 4 * kq;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        if (LN_IN)
+          av[rt][j] = *reinterpret_cast<const floatx4*>(&arows[(rt * kRT + c) * AS + kb0 + 16 * (b + j) + 4 * kq]);
+        else
+          av[rt][j] = (MQ_ROWS_DBG & 2) ? floatx4{0.1f, 0.2f, 0.3f, 0.4f}
+                                        : *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
+      }
     }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        if (MQ_ROWS_DBG & 4)
-          acc[t] += av[j][t] * wv[j][t];
-        else
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][t], wv[j][t], acc, 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          if (MQ_ROWS_DBG & 4)
+            acc[rt][t] += av[rt][j][t] * wv[j][t];
+          else
+            acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[rt][j][t], wv[j][t], acc[rt], 0, 0, 0);
+        }
       }
     }
   }
+  KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 3);
   // accumulator element j is (row 4 kq + j, column c) of this wave's partial tile
 #pragma unroll
-  for (int j = 0; j < 4; ++j) part[wave][(4 * kq + j) * kRT + c] = acc[j];
-  __syncthreads();
-  if (et >= kRT * kRT) return;
-  float v = part[0][et];
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-  for (int w = 1; w < kRWaves; ++w) v += part[w][et];
+    for (int j = 0; j < 4; ++j) part[wave][rt][(4 * kq + j) * kRT + c] = acc[rt][j];
+  __syncthreads();
+  KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 4);
+  if (ert >= RT) return;
+  float v = part[0][ert][ee];
+#pragma unroll
+  for (int w = 1; w < kRWaves; ++w) v += part[w][ert][ee];
   if (erow >= M) return;
   if (ks == 0) {  // split 0 carries bias / residual; GELU needs an unsplit K
     v += ebias;
@@ -543,6 +592,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     if (EPI == EPI_RESID) v += eres;
   }
   out[ks * o_plane + (int64_t)erow * ldo + ecol] = v;
+  KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 5);
 }
 
 // One wave per row of H = 256*VPL floats held in registers (two-pass mean/variance).
@@ -847,6 +897,179 @@ __global__ __launch_bounds__(512) void attention_rows_kernel(const float* __rest
   }
 }
 
+// K3o: attention + output projection of the few-row forward in ONE launch (L <= 64 keys;
+// one attention launch per layer fewer).  Workgroup (column tile, query tile, head group):
+// 8 waves; waves 0..HG-1 each run one head of the group for the tile's <= 16 queries of
+// one sequence (all its keys), as attention_rows_kernel does on v_mfma_f32_16x16x4_f32 but
+// with the whole key range in one wave (softmax max / sum by two cross-lane-group
+// shuffles, no LDS exchange), and leave ctx[query][head group's 64 HG dims] in LDS; then
+// all 8 waves multiply it by the group's K slice of Wo^T for the tile's 32 output columns
+// (2 column blocks x 4 K quarters, partial tiles summed in order through LDS).  Group g
+// writes output plane g (planes = heads / HG; the next FFN-up sums them while it
+// normalises, as QKV sums FFN-down's split-K planes); plane 0 carries bias + residual.
+// The attention of a query tile is recomputed by each of the H / 32 column tiles: HG heads
+// x 16 queries x L keys of f32 MFMA per workgroup (~1.5 us at L = 32), cheaper than the
+// separate launch and its boundary it replaces.
+// Rows: output row r of the projection is query position q = r % rps of sequence
+// b = r / rps (rps = L, or 1 for the CLS-only last layer: query 0, compact rows).
+constexpr int kOpCols = 32;  // output columns per workgroup
+
+template <int HG, int NKB>
+__global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
+    const float* __restrict__ qkv, const int* __restrict__ mask, int L, int H, int rps, int qtiles,
+    float scale, const float* __restrict__ Wo, const float* __restrict__ bo,
+    const float* __restrict__ resid, int ldr, float* __restrict__ out, int64_t o_plane) {
+  // NKB = ceil(L / 16) key blocks (compile time: every operand load below is issued before
+  // the first MFMA, one memory round trip for the whole launch)
+  constexpr int KG = HG * kDh;     // K depth of this group's slice of the projection
+  constexpr int CS = KG + 4;       // LDS row stride of ctx (conflict-free ds_read_b128)
+  constexpr int KQ = KG / 4;       // K per quarter
+  constexpr int NJ = KQ / 16;      // float4 per lane per operand in a quarter
+  __shared__ __attribute__((aligned(16))) float ctx[16 * CS];
+  __shared__ float part[8][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y / qtiles, q0 = (blockIdx.y % qtiles) * 16;
+  const int grp = blockIdx.z, h0 = grp * HG;
+  const int n0 = blockIdx.x * kOpCols;
+  const int64_t srow0 = (int64_t)b * L;  // first qkv row of the sequence
+  const int ld = 3 * H;
+
+  KTRACE_R(3, 0);
+  // projection operands of phase B, in flight from the start: wave w = (column block cb,
+  // K quarter kqr); lane (c, g) holds W[n0 + 16 cb + c][k] at k = kqr KQ + 16 j + 4 g + t
+  const int cb = w & 1, kqr = w >> 1;
+  floatx4 wv[NJ];
+  {
+    const float* wrow = Wo + (int64_t)(n0 + cb * 16 + c) * H + h0 * kDh + kqr * KQ + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+  }
+  // epilogue element of threads < 512: column block et >> 8, row (et & 255) / 16
+  const int et = threadIdx.x, ecb = et >> 8, erow_t = (et & 255) >> 4, ecol = n0 + ecb * 16 + (et & 15);
+  const int qrow = q0 + erow_t;  // query position of the element's row within the sequence
+  const int64_t orow = (int64_t)b * rps + qrow;
+  float ebias = 0.f, eres = 0.f;
+  if (grp == 0 && qrow < rps) {
+    ebias = bo[ecol];
+    eres = resid[orow * ldr + ecol];
+  }
+
+  if (w < HG) {
+    const int h = h0 + w;
+    // operands, all requested up front: Q (d = 16 s + 4 g + t for query c; rps == 1:
+    // query 0), K per key block (key 16 kb + c), V^T per key block (key 16 kb + 4 g + t,
+    // d = 16 db + c), the key mask
+    const int qpos = rps == 1 ? 0 : min(q0 + c, L - 1);
+    floatx4 qf[4], kf[NKB][4];
+    float vf[NKB][4][4];
+    const float* qs = qkv + (srow0 + qpos) * ld + h * kDh + 4 * g;
+#pragma unroll
+    for (int sI = 0; sI < 4; ++sI) qf[sI] = *reinterpret_cast<const floatx4*>(qs + 16 * sI);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      const float* ks = qkv + (srow0 + min(kb * 16 + c, L - 1)) * ld + H + h * kDh + 4 * g;
+#pragma unroll
+      for (int sI = 0; sI < 4; ++sI) kf[kb][sI] = *reinterpret_cast<const floatx4*>(ks + 16 * sI);
+    }
+    const float* vs = qkv + srow0 * ld + 2 * H + h * kDh + c;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int64_t kk = min(kb * 16 + 4 * g + t, L - 1);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) vf[kb][db][t] = vs[kk * ld + 16 * db];
+      }
+    const bool kval = lane < L && mask[srow0 + min(lane, L - 1)] != 0;
+    const unsigned long long kbits = __ballot(kval);  // bit k: key k usable
+#pragma unroll
+    for (int sI = 0; sI < 4; ++sI) qf[sI] *= scale;
+    KTRACE_R(3, 1);  // operands landed
+    floatx4 st[NKB];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kb][0][t], qf[0][t], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kb][2][t], qf[2][t], a1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kb][1][t], qf[1][t], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kb][3][t], qf[3][t], a1, 0, 0, 0);
+      }
+      st[kb] = a0 + a1;  // st[kb][j] = S^T[key 16 kb + 4 g + j][query c]
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kb * 16 + 4 * g + j;
+        st[kb][j] = ((kbits >> key) & 1ull) ? st[kb][j] : -INFINITY;
+        mx = fmaxf(mx, st[kb][j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st[kb][j] = (st[kb][j] == -INFINITY) ? 0.f : expf(st[kb][j] - mx);
+        ls += st[kb][j];
+      }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    const float inv = ls > 0.f ? 1.0f / ls : 0.f;
+    // O^T[d][query] = V^T P^T: A = V[key 16 kb + 4 g + t][d = 16 db + c], B = st[kb][t]
+    floatx4 o[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      o[db] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[kb][db][t], st[kb][t], o[db], 0, 0, 0);
+    }
+    // o[db][j] = O^T[d = 16 db + 4 g + j][query c]
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ctx[c * CS + w * kDh + 16 * db + 4 * g + j] = o[db][j] * inv;
+    KTRACE_R(3, 2);  // attention done (wave 0)
+  }
+  __syncthreads();
+  KTRACE_R(3, 3);
+  // phase B: partial [16 rows][16 cols] of column block cb over K quarter kqr, as two
+  // interleaved accumulation chains (one chain of NJ * 4 dependent MFMAs waits out each
+  // one's latency)
+  floatx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const floatx4 av = *reinterpret_cast<const floatx4*>(&ctx[c * CS + kqr * KQ + 16 * j + 4 * g]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc2[j & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], wv[j][t], acc2[j & 1], 0, 0, 0);
+  }
+  const floatx4 acc = acc2[0] + acc2[1];
+  KTRACE_R(3, 4);
+  // acc[j] = (row 4 g + j, column c) of the partial
+#pragma unroll
+  for (int j = 0; j < 4; ++j) part[w][(4 * g + j) * 16 + c] = acc[j];
+  __syncthreads();
+  KTRACE_R(3, 5);
+  const int e = et & 255;
+  float v = part[ecb][e];
+#pragma unroll
+  for (int q = 1; q < 4; ++q) v += part[ecb + 2 * q][e];
+  if (qrow >= rps) return;
+  if (grp == 0) v = (v + ebias) + eres;
+  out[grp * o_plane + orow * H + ecol] = v;
+  KTRACE_R(3, 6);
+}
+
 // --------------------------------------------------------------- K7 pool -----
 // One wave per sequence: CLS row (or masked mean over rows), then x / max(||x||, 1e-12).
 template <int VPL>
@@ -1043,7 +1266,7 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
 
 // Split-K factor for a GEMM that would under-fill the chip (0 = run it directly):
 // enough chunks for ~2 workgroups per CU, each chunk a multiple of 32 deep.
-int splitk_factor(const GemmArgs& g, int num_cus) {
+int splitk_factor(const GemmArgs& g, int num_cus, int cap = 16) {
   if (!g.slab || g.N % 4 != 0) return 0;
   const int64_t tiles = (int64_t)((g.M + 31) / 32) * ((g.N + 127) / 128);  // 32 x 128 tiles
   const int64_t slots = 2 * (int64_t)num_cus;
@@ -1051,11 +1274,7 @@ int splitk_factor(const GemmArgs& g, int num_cus) {
   const int slices = g.K / kBK;
   // At most 16 chunks: deeper splits fill more CUs but the slab traffic and the ordered
   // reduction grow with S (single query, L=32: encoder p50 0.74 ms at 16 vs 0.88 ms at
-  // 64, 0.80 ms at 8).  MQ_SPLITK_MAX overrides it for tuning.
-  static const int cap = [] {
-    const char* v = getenv("MQ_SPLITK_MAX");
-    return v && atoi(v) >= 2 ? atoi(v) : 16;
-  }();
+  // 64, 0.80 ms at 8).  MQ_ENC_OPT_SPLITK_MAX overrides it.
   int best = 1;
   for (int s = 1; s <= slices && s <= cap; ++s)
     if (slices % s == 0 && tiles * s <= slots && (size_t)s * g.M * g.N <= g.slab_floats) best = s;
@@ -1074,8 +1293,8 @@ void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
 }
 
 template <int EPI>
-void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false) {
-  const int S = splitk_factor(g, num_cus);
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false, int splitk_cap = 16) {
+  const int S = splitk_factor(g, num_cus, splitk_cap);
   if (S) {
     launch_splitk<EPI>(g, S, s);
     return;
@@ -1146,6 +1365,12 @@ struct mq_encoder {
     uint64_t last_use = 0;
   };
   std::vector<Graph> graphs;
+  // tuning options (mq_encoder_set_option)
+  bool fuse_attn_oproj = true;  // few-row forward: K3o (attention + output projection)
+  int rows_max = kRowsDefault;  // few-row forward up to this many token rows (0 = off)
+  int rows_splits = 0;          // few-row FFN-down K splits (0 = automatic)
+  int splitk_max = 16;          // deepest split-K of the tiled path's few-row GEMMs
+  int ln_rows_per_wave = 4;     // batched LayerNorm kernel: rows per wave
   bool use_graphs = false;  // eager measured faster for one query (0.628 vs 0.645 ms: the
                             // graph path stages ids / mask / out through its own buffers)
   uint64_t graph_clock = 0;
@@ -1158,7 +1383,7 @@ namespace {
 template <int EPI>
 void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6);
+  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6, e->splitk_max);
 }
 
 // Residual projection + LayerNorm: x = LN(A W^T + b + resid), through y (g.out) on the
@@ -1170,7 +1395,7 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
                    int stage, hipStream_t s) {
   const int H = VPL * 256;
   const unsigned rb = (unsigned)((g.M + 3) / 4);
-  const int S = splitk_factor(g, e->num_cus);
+  const int S = splitk_factor(g, e->num_cus, e->splitk_max);
   if (S && g.ldr == H && g.N == H) {
     using T = F32Tile<1, 4, 1, 1>;
     e->tl.mark(s, stage);
@@ -1184,10 +1409,7 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
   }
   gemm<EPI_RESID>(e, g, stage, s);
   e->tl.mark(s, ST_LN);
-  static const int rpw = [] {  // rows per wave (A/B knob MQ_LN_RPW = 1 / 2 / 4)
-    const char* v = getenv("MQ_LN_RPW");
-    return v ? atoi(v) : 4;
-  }();
+  const int rpw = e->ln_rows_per_wave;  // MQ_ENC_OPT_LN_ROWS_PER_WAVE: 1 / 2 / 4
   if (rpw == 4)
     hipLaunchKernelGGL((ln_kernel<VPL, 4>), dim3((unsigned)((g.M + 15) / 16)), dim3(256), 0, s, g.out, g.M, lng,
                        lnb, e->cfg.ln_eps, x);
@@ -1278,13 +1500,31 @@ struct RowsArgs {
   const float* typ = nullptr;
 };
 
+// Row tiles per workgroup: two for the LayerNorm-input GEMMs when M > 16 (the launch then
+// streams each weight panel once instead of once per 16-row tile: QKV 10.5 -> 9.0 us,
+// FFN-up 10.1 -> 8.6 us at M = 32), unless the normalised rows would not fit LDS (hidden
+// 1024).  The plain GEMMs keep one: with half the workgroups their per-CU bytes, not the
+// chip's, bound them (FFN-down 7.8 -> 10.9 us with two).
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT>
+void launch_rows_rt(const RowsArgs& g, const float* lng, const float* lnb, float eps, float* ln_out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN, RT>),
+                     dim3(g.N / kRT, (g.M + kRT * RT - 1) / (kRT * RT), g.splits), dim3(64 * kRWaves), 0, s,
+                     g.A, g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
+                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ);
+}
+
 template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
 void launch_rows_nb(const RowsArgs& g, const float* lng, const float* lnb, float eps, float* ln_out,
                     hipStream_t s) {
-  hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN>),
-                     dim3(g.N / kRT, (g.M + kRT - 1) / kRT, g.splits), dim3(64 * kRWaves), 0, s, g.A,
-                     g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
-                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ);
+  constexpr bool two_fit = LN_IN && (size_t)(2 * kRT * (NB * 256 + 4) + kRWaves * 2 * kRT * kRT) * 4 <= 160 * 1024;
+  if constexpr (two_fit) {
+    if (g.M > kRT) {
+      launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 2>(g, lng, lnb, eps, ln_out, s);
+      return;
+    }
+  }
+  launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 1>(g, lng, lnb, eps, ln_out, s);
 }
 
 // Per-split depths the few-row kernel is instantiated for (K / 256 blocks per wave).
@@ -1294,12 +1534,8 @@ bool rows_nb_ok(int nb) { return nb >= 1 && (nb <= 4 || nb == 6 || nb == 8 || nb
 // More splits put more workgroups on the weights but add planes the consumer sums (at
 // K = 3072, encoder p50: one split 13.9 us per FFN-down launch; two 0.474 ms, three 0.495,
 // four 0.493 - FFN-down 8.9 / 9.2 / 7.1 us, the next QKV 9.2 / 10.0 / 11.0 us).
-int rows_splits(int K) {
+int rows_splits(int K, int forced = 0) {  // forced: MQ_ENC_OPT_ROWS_SPLITS, used when it divides K / 256
   const int nb = K / 256;
-  static const int forced = [] {  // A/B knob MQ_ROWS_SPLITS (used when it divides K / 256)
-    const char* v = getenv("MQ_ROWS_SPLITS");
-    return v ? atoi(v) : 0;
-  }();
   if (forced >= 1 && forced <= 4 && nb % forced == 0 && rows_nb_ok(nb / forced)) return forced;
   for (int sp = 1; sp <= 4; ++sp)
     if (nb % sp == 0 && nb / sp <= 6 && rows_nb_ok(nb / sp)) return sp;
@@ -1340,6 +1576,40 @@ void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* 
   }
 }
 
+template <int HG>
+void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
+                          int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
+                          int ldr, float* out, int64_t o_plane) {
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(512), 0, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out,
+                       o_plane);
+  };
+  switch (nkb) {
+    case 1: go(attn_oproj_rows_kernel<HG, 1>); break;
+    case 2: go(attn_oproj_rows_kernel<HG, 2>); break;
+    case 3: go(attn_oproj_rows_kernel<HG, 3>); break;
+    default: go(attn_oproj_rows_kernel<HG, 4>); break;
+  }
+}
+
+void launch_attn_oproj(int hg, int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
+                       int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid, int ldr,
+                       float* out, int64_t o_plane) {
+  if (hg == 6)
+    launch_attn_oproj_hg<6>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane);
+  else
+    launch_attn_oproj_hg<4>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane);
+}
+
+// Heads per output plane of the fused attention + output projection (K3o), 0 = run
+// attention and the projection as two launches (keys past 64, or a head count neither
+// 6 nor 4 divides).  6 at BERT-base (12 heads: two planes).
+int oproj_heads_per_plane(const mq_encoder* e, int L) {
+  const mq_bert_config& c = e->cfg;
+  if (!e->fuse_attn_oproj || L > 64 || c.hidden != c.heads * kDh || c.hidden % kOpCols) return 0;
+  return c.heads % 6 == 0 ? 6 : c.heads % 4 == 0 ? 4 : 0;
+}
+
 // Few-row forward (B * L <= kRowsMax): 5 launches per layer instead of 9, 5 L + 1 in all.  Between
 // layers the activations stay pre-LayerNorm, as the FFN-down's split-K planes in `slab`;
 // the next GEMM sums and normalises them on load (K2r LN_IN) and materialises the
@@ -1360,7 +1630,8 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
   const float eps = c.ln_eps;
   const float scale = 1.0f / sqrtf((float)(H / c.heads));
   const int q_tiles = (L + 31) / 32;
-  const int dsplit = rows_splits(F);
+  const int dsplit = rows_splits(F, e->rows_splits);
+  const int hg = oproj_heads_per_plane(e, L);
   int prev_rows = M;
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
@@ -1382,22 +1653,32 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
                                      3 * H, 0, M, 3 * H, H, 1},
                                     dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
     }
-    e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
-    if (L <= 64)
-      hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
-                         H, c.heads, qt, scale, e->ctx.p);
-    else
-      hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L, H,
-                         c.heads, qt, scale, e->ctx.p);
-    e->tl.mark(s, ST_OPROJ);
-    launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
+    int y_planes = 1;
+    if (hg) {  // attention + output projection in one launch (K3o), hg heads per plane
+      e->tl.mark(s, ST_OPROJ);
+      const int rps = cls_only ? 1 : L, qtiles = (rps + 15) / 16;
+      y_planes = c.heads / hg;
+      const dim3 grid(H / kOpCols, B * qtiles, y_planes);
+      launch_attn_oproj(hg, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wo, w.bo, e->x.p,
+                        stride, e->y.p, (int64_t)rows * H);
+    } else {
+      e->tl.mark(s, ST_ATTN);
+      if (L <= 64)
+        hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
+                           H, c.heads, qt, scale, e->ctx.p);
+      else
+        hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L, H,
+                           c.heads, qt, scale, e->ctx.p);
+      e->tl.mark(s, ST_OPROJ);
+      launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
+    }
     e->tl.mark(s, ST_FFN_UP);
-    const RowsArgs up{e->y.p, H, 0, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
+    const RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
     if (c.gelu == MQ_GELU_TANH)
-      launch_rows_ln<EPI_GELU_TANH, VPL>(up, 1, w.ln1g, w.ln1b, eps, e->x.p, s);
+      launch_rows_ln<EPI_GELU_TANH, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     else
-      launch_rows_ln<EPI_GELU_ERF, VPL>(up, 1, w.ln1g, w.ln1b, eps, e->x.p, s);
+      launch_rows_ln<EPI_GELU_ERF, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     e->tl.mark(s, ST_FFN_DOWN);
     launch_rows<EPI_RESID>({e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F,
                             dsplit},
@@ -1414,20 +1695,14 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
   return MQ_OK;
 }
 
-// The few-row forward serves B * L <= kRowsMax token rows (a single query up to 64
-// tokens); MQ_ROWS_PATH=0 turns it off (A/B measurements).
+// The few-row forward serves B * L <= rows_max token rows (MQ_ENC_OPT_ROWS_MAX, default
+// 64: a single query up to 64 tokens; 0 turns it off).
 bool use_rows_path(const mq_encoder* e, int B, int L) {
-  static const int rows_max = [] {
-    const char* v = getenv("MQ_ROWS_PATH");
-    if (v && v[0] == '0') return 0;
-    const char* m = getenv("MQ_ROWS_MAX");
-    return m ? std::min(atoi(m), kRowsMax) : kRowsDefault;
-  }();
   const mq_bert_config& c = e->cfg;
+  const int sp = rows_splits(c.ffn, e->rows_splits);
   // slab holds the FFN-down planes: splits x rows x H floats
-  return (int64_t)B * L <= rows_max && !e->layers.empty() && c.ffn % 256 == 0 &&
-         rows_nb_ok(c.ffn / 256 / rows_splits(c.ffn)) &&
-         (size_t)rows_splits(c.ffn) * B * L * c.hidden <= e->slab.n;
+  return (int64_t)B * L <= e->rows_max && !e->layers.empty() && c.ffn % 256 == 0 &&
+         rows_nb_ok(c.ffn / 256 / sp) && (size_t)sp * B * L * c.hidden <= e->slab.n;
 }
 
 }  // namespace
@@ -1656,6 +1931,54 @@ int mq_encoder_set_graphs(mq_encoder* e, int enabled) {
   return MQ_OK;
 }
 
+int mq_encoder_set_option(mq_encoder* e, int option, int value) {
+  clear_error();
+  MQ_CHECK_ARG(e, "NULL encoder");
+  std::lock_guard<std::mutex> lk(e->mu);
+  switch (option) {
+    case MQ_ENC_OPT_ROWS_MAX:
+      MQ_CHECK_ARG(value >= 0 && value <= kRowsMax, "rows_max must be in [0, %d] (got %d)", kRowsMax, value);
+      e->rows_max = value;
+      break;
+    case MQ_ENC_OPT_ROWS_SPLITS:
+      MQ_CHECK_ARG(value >= 0 && value <= 4, "rows_splits must be in [0, 4] (got %d)", value);
+      e->rows_splits = value;
+      break;
+    case MQ_ENC_OPT_SPLITK_MAX:
+      MQ_CHECK_ARG(value >= 2 && value <= 64, "splitk_max must be in [2, 64] (got %d)", value);
+      e->splitk_max = value;
+      break;
+    case MQ_ENC_OPT_LN_ROWS_PER_WAVE:
+      MQ_CHECK_ARG(value == 1 || value == 2 || value == 4, "ln_rows_per_wave must be 1, 2 or 4 (got %d)", value);
+      e->ln_rows_per_wave = value;
+      break;
+    case MQ_ENC_OPT_FUSE_ATTN_OPROJ:
+      MQ_CHECK_ARG(value == 0 || value == 1, "fuse_attn_oproj must be 0 or 1 (got %d)", value);
+      e->fuse_attn_oproj = value != 0;
+      break;
+    default:
+      MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
+  }
+  // captured forwards bake the old choices in
+  for (auto& g : e->graphs) (void)hipGraphExecDestroy(g.exec);
+  e->graphs.clear();
+  return MQ_OK;
+}
+
+int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
+  clear_error();
+  MQ_CHECK_ARG(e && value, "NULL argument");
+  switch (option) {
+    case MQ_ENC_OPT_ROWS_MAX: *value = e->rows_max; break;
+    case MQ_ENC_OPT_ROWS_SPLITS: *value = e->rows_splits; break;
+    case MQ_ENC_OPT_SPLITK_MAX: *value = e->splitk_max; break;
+    case MQ_ENC_OPT_LN_ROWS_PER_WAVE: *value = e->ln_rows_per_wave; break;
+    case MQ_ENC_OPT_FUSE_ATTN_OPROJ: *value = e->fuse_attn_oproj ? 1 : 0; break;
+    default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
+  }
+  return MQ_OK;
+}
+
 int mq_encoder_set_timing(mq_encoder* e, int enabled) {
   clear_error();
   MQ_CHECK_ARG(e, "NULL encoder");
@@ -1695,7 +2018,8 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   // split-K slabs: up to 2*CUs partial tiles of 32 x 128 floats
   rc = e->slab.ensure((size_t)2 * e->num_cus * 32 * 128);
   if (rc) return rc;
-  for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, M * c.hidden),
+  // y also holds the few-row forward's output-projection planes (<= 4 of M rows)
+  for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, (M <= (size_t)kRowsMax ? 4 : 1) * M * c.hidden),
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
                   std::make_pair(&e->ffn, M * c.ffn)}) {
     rc = bn.first->ensure(bn.second);
@@ -1739,5 +2063,17 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   }
   return MQ_OK;
 }
+
+#ifdef MQ_KTRACE
+// Measurement builds: copy (and clear) the few-row kernels' phase stamps, [4][1024][8] int64.
+int mq_debug_ktrace_read(long long* out, int n) {
+  const int total = kTraceRegions * kTraceWgs * kTraceSlots;
+  if (!out || n < total) return MQ_EINVAL;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mq_ktrace), total * sizeof(long long)) != hipSuccess) return MQ_EHIP;
+  std::vector<long long> zero(total, 0);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mq_ktrace), zero.data(), total * sizeof(long long)) != hipSuccess) return MQ_EHIP;
+  return MQ_OK;
+}
+#endif
 
 }  // extern "C"

@@ -8,6 +8,9 @@
                    // only, 4 = no fragment reads, 8 = no barrier
 #define MQ_TS_DBG 0
 #endif
+#if MQ_TS_DBG != 0 && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_TS_DBG computes wrong results: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
+#endif
 #include "thresh.hpp"
 #include "topk.hpp"
 

@@ -20,6 +20,9 @@ MQ_DTYPE_F32, MQ_DTYPE_BF16, MQ_DTYPE_F32X6, MQ_DTYPE_F32_SCREEN = 0, 1, 2, 3
 MQ_GELU_ERF, MQ_GELU_TANH = 0, 1
 MQ_POOL_CLS, MQ_POOL_MEAN = 0, 1
 MQ_MAX_K = 64
+# mq_encoder_set_option ids (include/mq.h)
+MQ_ENC_OPT_ROWS_MAX, MQ_ENC_OPT_ROWS_SPLITS, MQ_ENC_OPT_SPLITK_MAX = 0, 1, 2
+MQ_ENC_OPT_LN_ROWS_PER_WAVE, MQ_ENC_OPT_FUSE_ATTN_OPROJ = 3, 4
 
 
 class MQError(RuntimeError):
@@ -80,6 +83,8 @@ SIGNATURES = {
     "mq_encoder_load_weights": (_I, [_P, _P, _I64]),
     "mq_encoder_set_precision": (_I, [_P, _I]),
     "mq_encoder_set_graphs": (_I, [_P, _I]),
+    "mq_encoder_set_option": (_I, [_P, _I, _I]),
+    "mq_encoder_get_option": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int)]),
     "mq_encoder_set_timing": (_I, [_P, _I]),
     "mq_encoder_read_timing": (_I, [_P, _P, _I]),
     "mq_encoder_embed": (_I, [_P, _P, _P, _I, _I, _P, _I, _P]),

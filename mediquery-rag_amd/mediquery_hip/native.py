@@ -211,6 +211,20 @@ class Encoder:
         MI355X for one query; bit-identical results)."""
         _lib.call("mq_encoder_set_graphs", self._h, int(bool(enabled)))
 
+    OPTIONS = {"rows_max": _lib.MQ_ENC_OPT_ROWS_MAX, "rows_splits": _lib.MQ_ENC_OPT_ROWS_SPLITS,
+               "splitk_max": _lib.MQ_ENC_OPT_SPLITK_MAX, "ln_rows_per_wave": _lib.MQ_ENC_OPT_LN_ROWS_PER_WAVE,
+               "fuse_attn_oproj": _lib.MQ_ENC_OPT_FUSE_ATTN_OPROJ}
+
+    def set_option(self, name, value):
+        """Tuning option of the forward (mq_encoder_set_option): rows_max, rows_splits,
+        splitk_max, ln_rows_per_wave, fuse_attn_oproj."""
+        _lib.call("mq_encoder_set_option", self._h, self.OPTIONS[name], int(value))
+
+    def get_option(self, name):
+        v = ctypes.c_int()
+        _lib.call("mq_encoder_get_option", self._h, self.OPTIONS[name], ctypes.byref(v))
+        return v.value
+
     def embed(self, ids, mask):
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         mask = np.ascontiguousarray(mask, dtype=np.int32)

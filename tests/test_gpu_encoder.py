@@ -153,3 +153,31 @@ def test_errors(require_gpu):
     with pytest.raises(_lib.MQError, match="max_positions"):
         enc.embed(np.zeros((1, 65), np.int32), np.ones((1, 65), np.int32))
     assert enc.embed(np.zeros((0, 8), np.int32), np.zeros((0, 8), np.int32)).shape == (0, 768)
+
+
+@pytest.mark.parametrize("name,value,B,L", [
+    ("rows_max", 0, 1, 32),        # one query through the tiled / split-K path
+    ("rows_max", 256, 2, 100),     # 200 token rows through the few-row forward
+    ("rows_splits", 1, 1, 32), ("rows_splits", 3, 2, 20), ("rows_splits", 4, 1, 48),
+    ("splitk_max", 4, 1, 32), ("splitk_max", 64, 1, 40),   # (with rows_max 0 below)
+    ("ln_rows_per_wave", 1, 9, 33), ("ln_rows_per_wave", 2, 9, 33),
+    ("fuse_attn_oproj", 0, 1, 32), ("fuse_attn_oproj", 0, 2, 17),
+])
+def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
+    """Every non-default value of the explicit tuning options (mq_encoder_set_option,
+    which replaced the old environment knobs) keeps the forward within the parity
+    tolerance of the oracle; the option reads back, bad values raise."""
+    cfg = BertConfig(layers=2)
+    rng = np.random.default_rng(L)
+    ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    mask[-1, L // 2:] = 0
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    enc = Encoder(cfg)
+    if name == "splitk_max":
+        enc.set_option("rows_max", 0)
+    enc.set_option(name, value)
+    assert enc.get_option(name) == value
+    _close(enc.embed(ids, mask), ref)
+    with pytest.raises(_lib.MQError):
+        enc.set_option(name, 1000)

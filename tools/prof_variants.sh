@@ -1,5 +1,5 @@
 # Kernel-trace the single-query encoder for the in-tree library and variants/*.so builds
-# (measurement builds, e.g. -DMQ_ROWS_DBG): per-kernel durations under gpurun_out/pv_<name>.
+# (measurement builds, e.g. -DMQ_MEASUREMENT_BUILD -DMQ_ROWS_DBG=1): per-kernel durations under gpurun_out/pv_<name>.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/gpurun_out

@@ -53,13 +53,62 @@ def counters(d):
     return out, dur
 
 
+def dispatches(d, counter):
+    """[(dispatch id, kernel, grid size, value of `counter`)] in dispatch order."""
+    path = find(d, "counter_collection.csv")
+    rows = []
+    if not path:
+        return rows
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            grid = r.get("Grid_Size") or r.get("Grid_Size_X") or ""
+            rows.append((int(r["Dispatch_Id"]), short(r["Kernel_Name"]), grid, float(r["Counter_Value"])))
+    rows.sort()
+    return rows
+
+
+def classify(rows):
+    """Dispatch -> bench.py kernel class, or None.  The encoder GEMM classes are the
+    headline shape's launches only: a class's most common grid (the full-M launches of
+    the L = 32 batch; the CLS-only last layer and other shapes drop out), and the shared
+    residual-epilogue instantiation is split by what precedes it (attention -> out-proj,
+    FFN-up -> FFN-down)."""
+    out = []
+    prev = ""
+    for did, k, grid, v in rows:
+        cls = None
+        if re.search(r"gemm_nt_kernel<.*false>, 0>", k):
+            cls = "qkv_gemm"
+        elif re.search(r"gemm_nt_kernel<.*false>, [12]>", k):
+            cls = "ffn_up_gemm"
+        elif re.search(r"gemm_nt_kernel<.*false>, 3>", k):
+            cls = "out_proj_gemm" if "attention" in prev else "ffn_down_gemm" if "gemm_nt_kernel" in prev else None
+        else:
+            for c, pat in CLASSES.items():
+                if c not in ("qkv_gemm", "ffn_up_gemm", "out_proj_gemm", "ffn_down_gemm") and re.search(pat, k):
+                    cls = c
+        out.append((cls, grid, v))
+        prev = k
+    by = defaultdict(lambda: defaultdict(list))
+    for cls, grid, v in out:
+        if cls:
+            by[cls][grid].append(v)
+    res = {}
+    for cls, grids in by.items():
+        grid, vals = max(grids.items(), key=lambda kv: len(kv[1]))
+        vals = sorted(vals)
+        res[cls] = (vals[len(vals) // 2], len(vals), grid)
+    return res
+
+
 def mean(v):
     return sum(v) / len(v) if v else 0.0
 
 
-# bench.py kernel class -> (kernel-name regex of its exact-f32 instantiations); when a
-# class has several instantiations (full-M and CLS-only), the largest per-launch
-# traffic is the full-M one
+# bench.py kernel class -> kernel-name regex (the encoder GEMM classes are resolved per
+# dispatch by classify())
 CLASSES = {
     "flat_search_kernel": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, false>, \d+>",
     "flat_search_kernel_x6": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, true, \d, false>, 8>",
@@ -128,17 +177,23 @@ def main():
                         "lds_bank_conflict_cycles"])
             w.writerows(srows)
 
-    if rows:
+    fcls = classify(dispatches(os.path.join(src, "fetch"), "FETCH_SIZE"))
+    wcls = classify(dispatches(os.path.join(src, "write"), "WRITE_SIZE"))
+    if fcls:
         traffic = {"note": "HBM bytes per launch = 2*FETCH_SIZE(KB)*1024 + WRITE_SIZE(KB)*1024 "
                            "(gfx950 FETCH_SIZE halves wide streaming reads, MI355X_MICROARCH.md "
-                           "HBM section); rocprofv3 --pmc passes of profiles/run_profiles.sh, "
-                           "summarised by tools/summarize_profiles.py; out_proj / ffn_down share "
-                           "one kernel instantiation (the larger per-launch figure is shown)",
-                   "source": dst}
-        for cls, pat in CLASSES.items():
-            vals = [r[4] for r in rows if re.search(pat, r[0])]
-            if vals:
-                traffic[cls] = max(vals)
+                           "HBM section), the median over the class's launches of the headline "
+                           "shape (its most common grid; out-proj / FFN-down told apart by the "
+                           "preceding launch); rocprofv3 --pmc passes of profiles/run_profiles.sh, "
+                           "summarised by tools/summarize_profiles.py",
+                   "source": dst, "launches": {}}
+        for cls, (fkb, n, grid) in sorted(fcls.items()):
+            wkb = wcls.get(cls, (0.0, 0, ""))[0]
+            traffic[cls] = int(2 * fkb * 1024 + wkb * 1024)
+            traffic["launches"][cls] = {"dispatches": n, "grid": grid, "fetch_kb": round(fkb, 1),
+                                        "write_kb": round(wkb, 1)}
+        with open(os.path.join(dst, "pmc_traffic_classes.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
         with open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json"), "w") as f:
             json.dump(traffic, f, indent=1)
     print("wrote", dst)
