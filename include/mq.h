@@ -196,12 +196,17 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *                                default 4)
  *   MQ_ENC_OPT_FUSE_ATTN_OPROJ   few-row forward: attention + output projection in one
  *                                launch (1, default) or two (0)
+ *   MQ_ENC_OPT_FUSED_LN          batched forward, exact f32, hidden <= 768: the residual
+ *                                projections (out-proj, FFN-down) on full-row tiles with
+ *                                the LayerNorm in their epilogue (1) or GEMM + LayerNorm
+ *                                launch (0, default: the full-row tiles measured slower)
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
 #define MQ_ENC_OPT_SPLITK_MAX 2
 #define MQ_ENC_OPT_LN_ROWS_PER_WAVE 3
 #define MQ_ENC_OPT_FUSE_ATTN_OPROJ 4
+#define MQ_ENC_OPT_FUSED_LN 5
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);

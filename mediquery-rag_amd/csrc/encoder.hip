@@ -128,6 +128,110 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
   walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
 }
 
+// ------------------------------------------- K4 / K6: residual GEMM + LayerNorm ---
+// x = LN(A W^T + bias + resid) with the LayerNorm in the epilogue: a workgroup owns 32 FULL
+// rows (BN = N = H, T = F32Tile<1, 8, 1, H / 256, ..., BK 16>: 8 waves x 32 x (H/8)
+// columns, 16-deep slices so the 32 + H row image double-buffers in LDS), so each row's
+// mean and variance are block reductions - no y round trip through HBM and no LayerNorm
+// launch (24 per batched step).  Two-pass statistics over the fp32 sums as ln_kernel
+// computes them (the summation order differs: results agree to rounding).  `out` may be
+// `resid` (each element is read and written by the same thread, and a workgroup owns its
+// rows); the strided CLS-only layer, whose compact output rows alias other residual rows,
+// keeps the two-launch path.  Persistent: workgroups walk row blocks t = blockIdx.x + i G.
+template <class T>
+__global__ __launch_bounds__(T::THREADS, 1) void gemm_resid_ln_kernel(
+    const float* __restrict__ A, int lda, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* resid, const float* __restrict__ lng, const float* __restrict__ lnb, float eps, float* out,
+    int M, int K) {
+  constexpr int H = T::BN;
+  static_assert(T::WAVES_M == 1 && T::TM == 1 && T::BM == 32, "32-row full-width tiles");
+  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
+  __shared__ float red[2][T::WAVES_N][32];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int total = (M + 31) / 32;
+  const int n_tiles = blockIdx.x < total ? (total - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+  auto coords = [&](int i, int& m0, int64_t& n0) {
+    m0 = (blockIdx.x + i * gridDim.x) * 32;
+    n0 = 0;
+  };
+  // this lane's columns: wave w, tile tn, lane & 31; bias / gamma / beta held for the launch
+  float bv[T::TN], gv[T::TN], ev[T::TN];
+#pragma unroll
+  for (int tn = 0; tn < T::TN; ++tn) {
+    const int col = wave * T::WN + tn * 32 + (lane & 31);
+    bv[tn] = bias[col];
+    gv[tn] = lng[col];
+    ev[tn] = lnb[col];
+  }
+  auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
+    const int m0 = (blockIdx.x + i * gridDim.x) * 32;
+    // v = acc + bias + resid (rows past M read row M - 1 and are never stored)
+#pragma unroll
+    for (int tn = 0; tn < T::TN; ++tn) {
+      const int col = wave * T::WN + tn * 32 + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = min(m0 + acc_row(0, e, lane), M - 1);
+        acc[0][tn][e] = acc[0][tn][e] + bv[tn] + resid[(int64_t)row * H + col];
+      }
+    }
+    // row sums: this lane's T::TN columns, then the 32 lanes of its half (same rows), then
+    // the waves through LDS; element e of lane half h is row (e&3) + 8(e>>2) + 4h
+    auto row_reduce = [&](int pass, auto&& val) {
+      float p[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn) t += val(tn, e);
+        p[e] = t;
+      }
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) p[e] += __shfl_xor(p[e], off);
+      if ((lane & 31) == 0)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[pass][wave][acc_row(0, e, lane)] = p[e];
+    };
+    row_reduce(0, [&](int tn, int e) { return acc[0][tn][e]; });
+    __syncthreads();
+    float mean[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rr = acc_row(0, e, lane);
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < T::WAVES_N; ++w) t += red[0][w][rr];
+      mean[e] = t * (1.0f / H);
+    }
+    row_reduce(1, [&](int tn, int e) {
+      const float d = acc[0][tn][e] - mean[e];
+      return d * d;
+    });
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rr = acc_row(0, e, lane);
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < T::WAVES_N; ++w) t += red[1][w][rr];
+      const float rstd = 1.0f / sqrtf(t * (1.0f / H) + eps);
+      const int row = m0 + rr;
+      if (row < M) {
+#pragma unroll
+        for (int tn = 0; tn < T::TN; ++tn) {
+          const int col = wave * T::WN + tn * 32 + (lane & 31);
+          out[(int64_t)row * H + col] = (acc[0][tn][e] - mean[e]) * rstd * gv[tn] + ev[tn];
+        }
+      }
+    }
+    // (the next tile's reductions reuse red[]: its first write follows a block barrier
+    // inside the slice loop, after every wave has read this tile's sums)
+  };
+  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, H, K}, coords, epi);
+}
+
 // ---------------------------------------------------------- split-K GEMM ------
 // For few rows (single queries, the CLS-only last layer) the direct GEMM leaves most
 // CUs idle.  Split K into S chunks: workgroup (tile, s) multiplies its tile over
@@ -1371,6 +1475,8 @@ struct mq_encoder {
   int rows_splits = 0;          // few-row FFN-down K splits (0 = automatic)
   int splitk_max = 16;          // deepest split-K of the tiled path's few-row GEMMs
   int ln_rows_per_wave = 4;     // batched LayerNorm kernel: rows per wave
+  bool fused_ln = false;        // batched residual GEMMs: LayerNorm in the epilogue (full-row tiles;
+                                // measured slower, kept as an option: DESIGN.md §4)
   bool use_graphs = false;  // eager measured faster for one query (0.628 vs 0.645 ms: the
                             // graph path stages ids / mask / out through its own buffers)
   uint64_t graph_clock = 0;
@@ -1396,6 +1502,19 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
   const int H = VPL * 256;
   const unsigned rb = (unsigned)((g.M + 3) / 4);
   const int S = splitk_factor(g, e->num_cus, e->splitk_max);
+  if constexpr (VPL <= 3) {  // (the 32 + H row image of hidden 1024 does not double-buffer in LDS)
+    // full-row tiles with the LayerNorm in the epilogue: exact f32, unit-stride residual
+    // rows written in place (the strided CLS-only layer's compact output would overwrite
+    // residual rows other workgroups still read)
+    if (!S && e->fused_ln && e->precision == MQ_DTYPE_F32 && g.ldr == H && g.N == H && g.resid == x) {
+      using T = F32Tile<1, 8, 1, VPL, false, 2, false, 16>;
+      e->tl.mark(s, stage);
+      const int tiles = (g.M + 31) / 32;
+      hipLaunchKernelGGL((gemm_resid_ln_kernel<T>), dim3(std::min(tiles, e->num_cus)), dim3(T::THREADS), 0, s,
+                         g.A, g.lda, g.W, g.bias, g.resid, lng, lnb, e->cfg.ln_eps, x, g.M, g.K);
+      return;
+    }
+  }
   if (S && g.ldr == H && g.N == H) {
     using T = F32Tile<1, 4, 1, 1>;
     e->tl.mark(s, stage);
@@ -1956,6 +2075,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value == 0 || value == 1, "fuse_attn_oproj must be 0 or 1 (got %d)", value);
       e->fuse_attn_oproj = value != 0;
       break;
+    case MQ_ENC_OPT_FUSED_LN:
+      MQ_CHECK_ARG(value == 0 || value == 1, "fused_ln must be 0 or 1 (got %d)", value);
+      e->fused_ln = value != 0;
+      break;
     default:
       MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
@@ -1974,6 +2097,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_SPLITK_MAX: *value = e->splitk_max; break;
     case MQ_ENC_OPT_LN_ROWS_PER_WAVE: *value = e->ln_rows_per_wave; break;
     case MQ_ENC_OPT_FUSE_ATTN_OPROJ: *value = e->fuse_attn_oproj ? 1 : 0; break;
+    case MQ_ENC_OPT_FUSED_LN: *value = e->fused_ln ? 1 : 0; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
   return MQ_OK;

@@ -35,7 +35,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
 template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2,
-          bool BF16_ = false>
+          bool BF16_ = false, int BK_ = 0>
 struct F32Tile {
   static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
   static constexpr bool X6 = X6_;
@@ -49,9 +49,14 @@ struct F32Tile {
   static constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   static constexpr int THREADS = WAVES_M * WAVES_N * kWave;
   static constexpr int ROWS = BM + BN;
-  static constexpr int BK = X6 ? 16 : 32;                 // K per staged slice
+  // K per staged slice: 32 (exact f32 / bf16 default), 16 (split f32; or an exact-f32 tile
+  // whose B panel is too tall for two 32-deep stages, e.g. the full-row 32 x 768 tile)
+  static constexpr int BK = BK_ ? BK_ : (X6 ? 16 : 32);
+  static_assert(BK == 32 || (BK == 16 && !BF16), "slice depth 32, or 16 for the f32 forms");
   static constexpr int F4_PER_ROW = BK / 4;               // float4 per row per slice
-  static constexpr int ROW_FLOATS = X6 ? 28 : kLdsStride; // LDS row stride in 4-B words
+  // LDS row stride in 4-B words: 144-B rows at BK 32, 80-B rows at BK 16 (16 rows of one
+  // ds_read_b128 group still land in distinct 16-B bank groups), 112-B split-plane rows
+  static constexpr int ROW_FLOATS = X6 ? 28 : BK + 4;
   static constexpr int TOTAL_F4 = ROWS * F4_PER_ROW;                  // float4 per slice
   static constexpr int LOADS = (TOTAL_F4 + THREADS - 1) / THREADS;      // per thread
   static constexpr bool PARTIAL = TOTAL_F4 % THREADS != 0;              // last slot ragged
@@ -60,7 +65,9 @@ struct F32Tile {
   // workgroups per CU the kernel is built for: 2 x 4 waves, or 1 x 8 waves (LDS)
   static constexpr int WG_PER_CU = THREADS == 256 ? 2 : 1;
   static_assert(BM % 32 == 0 && BN % 32 == 0, "block tile must be a multiple of 32");
-  static_assert((BM * F4_PER_ROW) % THREADS == 0, "A / B rows must not share a load slot");
+  // A rows fill whole load slots (compile-time A / B split) unless the A panel is smaller
+  // than one slot (the full-row 32 x H tile: 128 A float4 for 512 threads), then per thread
+  static constexpr bool A_SLOTS = (BM * F4_PER_ROW) % THREADS == 0;
 };
 
 // Exact 3-way bf16 split of 4 floats: returns plane p as 4 packed bf16 (2 dwords).
@@ -118,7 +125,9 @@ struct Stager {
       if (T::PARTIAL && i == T::LOADS - 1 && f >= T::TOTAL_F4) break;
       const int row = f / T::F4_PER_ROW, ch = f % T::F4_PER_ROW;
       const float* p;
-      if (i < T::BM * T::F4_PER_ROW / T::THREADS) {  // compile-time: A rows come first
+      const bool a_row = T::A_SLOTS ? i < T::BM * T::F4_PER_ROW / T::THREADS  // compile-time: A rows first
+                                    : f < T::BM * T::F4_PER_ROW;
+      if (a_row) {
         p = A + (int64_t)min(m0 + row, M - 1) * lda;
       } else {
         p = B + min(n0 + (int64_t)(row - T::BM), N - 1) * ldb;
@@ -212,8 +221,10 @@ __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T:
       }
     return;
   }
-  const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * 16;
-  const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * 16;
+  // lane half h carries k = h BK/2 + 4 q + s (q < BK / 8)
+  constexpr int QN = T::BK / 8;
+  const float* as = stage + (wm * T::WM + r) * T::ROW_FLOATS + h * (T::BK / 2);
+  const float* bs = stage + (T::BM + wn * T::WN + r) * T::ROW_FLOATS + h * (T::BK / 2);
   // Two fragment sets: the ds_reads of step q+1 go out under the MFMAs of step q.  Left
   // to itself the scheduler reads two steps at once into ONE register set, so the reads
   // of steps 2-3 wait (WAR) for the last MFMA of step 1 and the pipe idles for an LDS
@@ -233,9 +244,9 @@ __device__ __forceinline__ void mma_slice(const float* stage, floatx16 (&acc)[T:
   frag(0, a[0], b[0]);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < QN; ++q) {
     const int c = q & 1;
-    if (q + 1 < 4) frag(q + 1, a[c ^ 1], b[c ^ 1]);
+    if (q + 1 < QN) frag(q + 1, a[c ^ 1], b[c ^ 1]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 4; ++s)

@@ -149,10 +149,13 @@ class _MetaColumns:
                 values = col[1] if col is not None else []
                 ops = cond.items() if isinstance(cond, dict) else (("$eq", cond),)
                 for op, x in ops:
-                    pick = [c for c, v in enumerate(values) if _pred(op, v, x)]
-                    if _pred(op, None, x):
-                        pick.append(-1)
-                    out &= np.isin(codes, np.asarray(pick, np.int32)) if pick else False
+                    # admitted codes -> one table lookup per row; code -1 (key absent)
+                    # indexes the table's last entry
+                    lut = np.zeros(len(values) + 1, bool)
+                    lut[-1] = _pred(op, None, x)
+                    for cv, v in enumerate(values):
+                        lut[cv] = _pred(op, v, x)
+                    out &= lut[codes]
         return out
 
 

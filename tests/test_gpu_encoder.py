@@ -162,6 +162,7 @@ def test_errors(require_gpu):
     ("splitk_max", 4, 1, 32), ("splitk_max", 64, 1, 40),   # (with rows_max 0 below)
     ("ln_rows_per_wave", 1, 9, 33), ("ln_rows_per_wave", 2, 9, 33),
     ("fuse_attn_oproj", 0, 1, 32), ("fuse_attn_oproj", 0, 2, 17),
+    ("fused_ln", 1, 70, 32), ("fused_ln", 1, 9, 130),
 ])
 def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     """Every non-default value of the explicit tuning options (mq_encoder_set_option,
@@ -176,6 +177,8 @@ def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     enc = Encoder(cfg)
     if name == "splitk_max":
         enc.set_option("rows_max", 0)
+    if name == "ln_rows_per_wave":  # (the LayerNorm kernel runs on the unfused path)
+        enc.set_option("fused_ln", 0)
     enc.set_option(name, value)
     assert enc.get_option(name) == value
     _close(enc.embed(ids, mask), ref)

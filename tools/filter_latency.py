@@ -1,0 +1,67 @@
+"""Filtered vs unfiltered search latency at the VectorStore surface:
+`HipChroma.similarity_search_by_vector(q, k=5, filter=...)` over N synthetic rows whose
+metadata carries a 16-value `tag` and an integer `n`; the filter passes ~1/2 or ~1/16 of
+the rows.  Reports p50 ms for: no filter, a repeated filter (the gathered scratch index is
+reused), and a fresh filter every call (vectorised where-evaluation + device gather).
+
+  python tools/filter_latency.py [--rows 1000000] [--iters 50]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mediquery-rag_amd"), ROOT]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from mediquery_hip import synth  # noqa: E402
+from mediquery_hip.vectorstore import HipChroma  # noqa: E402
+
+
+def p50(fn, iters):
+    lat = []
+    for it in range(iters + 3):
+        a = time.perf_counter()
+        fn(it)
+        if it >= 3:
+            lat.append((time.perf_counter() - a) * 1e3)
+    return round(statistics.median(lat), 3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    n = args.rows
+    dev = torch.device("cuda", 0)
+    emb = torch.nn.functional.normalize(synth.corpus_device(n, 768, dev), dim=1).cpu().numpy()
+    rng = np.random.default_rng(0)
+    tags = rng.integers(0, 16, n)
+    metas = [{"tag": "t%d" % t, "n": int(i % 100)} for i, t in enumerate(tags)]
+    store = HipChroma(dim=768, auto_persist=False)
+    t0 = time.perf_counter()
+    store.add_embeddings(emb, ["doc %d" % i for i in range(n)], metas, ["id%d" % i for i in range(n)])
+    t_add = time.perf_counter() - t0
+    qs = emb[rng.integers(0, n, 64)] + 0.01 * rng.standard_normal((64, 768)).astype(np.float32)
+    out = {"rows": n, "add_s": round(t_add, 2)}
+    out["unfiltered_ms"] = p50(lambda i: store.similarity_search_by_vector(qs[i % 64], k=5), args.iters)
+    out["repeated_filter_half_ms"] = p50(
+        lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"n": {"$lt": 50}}), args.iters)
+    out["repeated_filter_16th_ms"] = p50(
+        lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"tag": "t3"}), args.iters)
+    out["fresh_filter_16th_ms"] = p50(
+        lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"tag": "t%d" % (i % 16)}), args.iters)
+    out["fresh_filter_half_ms"] = p50(
+        lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"n": {"$lt": 40 + i % 20}}), args.iters)
+    t0 = time.perf_counter()
+    store.delete(["id%d" % i for i in range(0, n, 1000)])
+    out["delete_1k_of_n_s"] = round(time.perf_counter() - t0, 3)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

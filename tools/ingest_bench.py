@@ -37,8 +37,10 @@ def main():
     lens = mask.sum(1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(0, len(texts), args.chunk):
+    for n, s in enumerate(range(0, len(texts), args.chunk)):
         ix.add(emb.embed_array(texts[s:s + args.chunk]))
+        if n % 25 == 24:  # progress (a long run must keep writing)
+            print("progress %d docs %.1f s" % (s + args.chunk, time.perf_counter() - t0), file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     flops = sum(DMETA_BASE.flops_per_sequence(int(L)) for L in lens)
