@@ -49,17 +49,24 @@ def main():
     ap.add_argument("--exact-direct", action="store_true", help="search with MQ_DTYPE_F32 (default: the screen)")
     ap.add_argument("--encoder-seq-lens", default="",
                     help="comma list: only the single-query encoder p50 at these token counts")
+    ap.add_argument("--rows-max", default="",
+                    help="comma list of MQ_ENC_OPT_ROWS_MAX values to compare in --encoder-seq-lens mode")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.encoder_seq_lens:
         enc = Encoder(DMETA_BASE, device=0)
         q = torch.empty((1, 768), device=dev)
         res = {}
-        for L in [int(x) for x in args.encoder_seq_lens.split(",")]:
-            ids_np, mask_np = synth.token_batch(1, L)
-            ids = torch.from_numpy(ids_np).to(dev)
-            mask = torch.from_numpy(mask_np).to(dev)
-            res["encoder_ms_L%d" % L] = p50(lambda: enc.embed_device(ids, mask, q), args.iters)
+        for rm in [int(x) for x in args.rows_max.split(",")] if args.rows_max else [None]:
+            tag = ""
+            if rm is not None:
+                enc.set_option("rows_max", rm)
+                tag = "_rowsmax%d" % rm
+            for L in [int(x) for x in args.encoder_seq_lens.split(",")]:
+                ids_np, mask_np = synth.token_batch(1, L)
+                ids = torch.from_numpy(ids_np).to(dev)
+                mask = torch.from_numpy(mask_np).to(dev)
+                res["encoder_ms_L%d%s" % (L, tag)] = p50(lambda: enc.embed_device(ids, mask, q), args.iters)
         print(res, flush=True)
         return
     corpus = synth.corpus_device(args.rows, 768, dev)
