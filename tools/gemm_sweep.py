@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--tiles", default=",".join(str(t) for t in TILES))
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 bias, 1 GELU erf, 2 GELU tanh, 3 residual)")
     args = ap.parse_args()
     shapes = {k: SHAPES[k] for k in args.shapes.split(",")}
     tiles = {int(t): TILES[int(t)] for t in args.tiles.split(",")}
@@ -33,6 +34,8 @@ def main():
         R = torch.randn(M, N, device=dev)
         out = torch.empty(M, N, device=dev)
         epi = 1 if name == "ffn_up" else (3 if name in ("out_proj", "ffn_down") else 0)
+        if args.epi >= 0:
+            epi = args.epi
         for t, tname in tiles.items():
             def run():
                 _lib.call("mq_debug_gemm_f32", _lib.ptr(A), _lib.ptr(W), _lib.ptr(b), _lib.ptr(R),
@@ -47,7 +50,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / n
-            res["%s/%s" % (name, tname)] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+            res["%s/%s/epi%d" % (name, tname, epi)] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
     print(json.dumps(res, indent=1))
     for k, v in res.items():
         print("%-32s %6.1f TF" % (k, v["tflops"]))

@@ -79,11 +79,11 @@ def classify(rows):
     prev = ""
     for did, k, grid, v in rows:
         cls = None
-        if re.search(r"gemm_nt_kernel<.*false>, 0>", k):
+        if re.search(EXACT_GEMM + r"0>", k):
             cls = "qkv_gemm"
-        elif re.search(r"gemm_nt_kernel<.*false>, [12]>", k):
+        elif re.search(EXACT_GEMM + r"[12]>", k):
             cls = "ffn_up_gemm"
-        elif re.search(r"gemm_nt_kernel<.*false>, 3>", k):
+        elif re.search(EXACT_GEMM + r"3>", k):
             cls = "out_proj_gemm" if "attention" in prev else "ffn_down_gemm" if "gemm_nt_kernel" in prev else None
         else:
             for c, pat in CLASSES.items():
@@ -107,12 +107,15 @@ def mean(v):
     return sum(v) / len(v) if v else 0.0
 
 
+# the exact-f32 encoder GEMM (X6 = false, BF16 = false, optional slice-depth parameter)
+# followed by its epilogue id
+EXACT_GEMM = r"gemm_nt_kernel<mq::F32Tile<\d+, \d+, \d+, \d+, false, \d+, false(, \d+)?>, "
 # bench.py kernel class -> kernel-name regex (the encoder GEMM classes are resolved per
 # dispatch by classify())
 CLASSES = {
-    "flat_search_kernel": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, false>, \d+>",
-    "flat_search_kernel_x6": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, true, \d, false>, 8>",
-    "flat_search_kernel_bf16": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, true>, 8>",
+    "flat_search_kernel": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, false(, \d+)?>, \d+>",
+    "flat_search_kernel_x6": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, true, \d, false(, \d+)?>, 8>",
+    "flat_search_kernel_bf16": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, true(, \d+)?>, 8>",
     "bf16_thresh_kernel": r"bf16_thresh_kernel<\d+, 1>",
     "bf16_thresh_sample": r"bf16_thresh_kernel<\d+, 0>",
     "i8_thresh_kernel": r"i8_thresh_kernel<\d, 1, 1>",
