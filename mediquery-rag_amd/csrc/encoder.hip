@@ -29,9 +29,34 @@ namespace mq {
 
 enum Epi { EPI_BIAS = 0, EPI_GELU_ERF = 1, EPI_GELU_TANH = 2, EPI_RESID = 3 };
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU, branch-free (it runs 64 times per lane in every FFN-up tile epilogue; ocml's erff
+// is ~50 VALU + a divergent branch per element and measured as the FFN-up epilogue's cost).
+// erf form: x * Phi(x), Phi(x) = 0.5 erfc(-x / sqrt 2), with erfc(z) for z = |x| / sqrt 2 from
+// the Chebyshev fit t * exp(-z^2 + P(t)), t = 1 / (1 + z / 2) (Numerical Recipes erfcc,
+// |relative error| < 1.2e-7 for all z >= 0): Phi = 1 - e / 2 for x >= 0, e / 2 below.  No
+// 1 + erf cancellation for negative x: max |error| vs float64 3.8e-7 over [-12, 12], relative
+// 1.7e-6 where |gelu| > 1e-3 (0.5 x (1 + erff) in fp32: 4.5e-7 and 5.1e-5).  v_rcp / v_exp
+// are the hardware 1-ulp forms.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.4426950408889634f);  // erfc(z)
+  return x * (x >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e);
+}
+// tanh form (llama.cpp's): 0.5 x (1 + tanh u) = x / (1 + exp(-2u)), u = sqrt(2/pi)(x + 0.044715 x^3)
 __device__ __forceinline__ float gelu_tanh(float x) {
-  return 0.5f * x * (1.0f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+  const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -2.8853900817779268f));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -788,19 +813,28 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 // Operand k-order: lane half h carries head dims 32h..32h+31 for QK^T (one contiguous
 // 128-B read per row per lane), and key (s&3) + 8(s>>2) + 4h at PV step s (the
 // accumulator row map).  Online softmax across 32-key tiles; masked keys weigh 0.
+// NS > 1 (few (sequence, head, query tile) triples with many keys: a long single query, the
+// CLS-only last layer): NS waves per workgroup split the key tiles (wave w takes tiles w,
+// w + NS, ...), each with its own running max / sum / O^T, merged through LDS at the end in
+// wave order: O = sum_w e^(m_w - m) O_w / sum_w e^(m_w - m) l_w (the same softmax; the
+// rescaling order differs from one wave walking every tile, results agree to rounding).
 constexpr int kDh = 64;
 
-__global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
-                                                       const int* __restrict__ mask, int L,
-                                                       int H, int heads, int q_tiles,
-                                                       float scale, float* __restrict__ ctx) {
-  // one LDS tile, used in turn to stage Q, each key tile's K, and the output: [32][68]
-  // rows for staging (a 16-lane ds_read_b128 group hits 16 distinct bank groups), [32][65]
-  // for the output
+template <int NS>
+__global__ __launch_bounds__(64 * NS) void attention_kernel(const float* __restrict__ qkv,
+                                                            const int* __restrict__ mask, int L,
+                                                            int H, int heads, int q_tiles,
+                                                            float scale, float* __restrict__ ctx) {
+  // one LDS tile per wave, used in turn to stage Q, each key tile's K, and the output:
+  // [32][68] rows for staging (a 16-lane ds_read_b128 group hits 16 distinct bank groups),
+  // [32][65] for the output
   constexpr int kSt = kDh + 4;
-  __shared__ __attribute__((aligned(16))) float tile[32 * kSt];
+  __shared__ __attribute__((aligned(16))) float tiles[NS][32 * kSt];
+  __shared__ float wmax[NS > 1 ? NS : 1][32], wsum[NS > 1 ? NS : 1][32];
+  const int wv = NS > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  float* tile = tiles[wv];
   float(*obuf)[kDh + 1] = reinterpret_cast<float(*)[kDh + 1]>(tile);
-  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
   const int bseq = blockIdx.x / (q_tiles * heads);
   const int q0 = qt * 32;
@@ -833,12 +867,12 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
 #pragma unroll
   for (int e = 0; e < 16; ++e) o0[e] = o1[e] = 0.f;
 
-  for (int k0 = 0; k0 < L; k0 += 32) {
+  for (int k0 = wv * 32; k0 < L; k0 += 32 * NS) {
     const int kr = min(k0 + r, L - 1);
     const bool kvalid = (k0 + r < L) && mask[row0 + kr] != 0;
     const unsigned long long kbits = __ballot(kvalid);  // bit j = key k0 + j usable
     float kf[32];
-    stage(k0, H + h * kDh);  // (one wave: its LDS reads of the last tile precede these writes)
+    stage(k0, H + h * kDh);  // (one wave per tile: its LDS reads of the last tile precede these writes)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const floatx4 v = *reinterpret_cast<const floatx4*>(&tile[r * kSt + hh * 32 + 4 * i]);
@@ -884,17 +918,62 @@ __global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__
       o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, st[sidx], o1, 0, 0, 0);
     }
   }
-  // O^T (d on registers, query on lanes) -> LDS [query][d] -> coalesced row stores
-  const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int d = (e & 3) + 8 * (e >> 2) + 4 * hh;
-    obuf[r][d] = o0[e] * inv;
-    obuf[r][d + 32] = o1[e] * inv;
-  }
-  __syncthreads();
   const int nrows = min(32, L - q0);
-  for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
+  if constexpr (NS == 1) {
+    // O^T (d on registers, query on lanes) -> LDS [query][d] -> coalesced row stores
+    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int d = (e & 3) + 8 * (e >> 2) + 4 * hh;
+      obuf[r][d] = o0[e] * inv;
+      obuf[r][d + 32] = o1[e] * inv;
+    }
+    __syncthreads();
+    for (int q = 0; q < nrows; ++q) ctx[(row0 + q0 + q) * H + h * kDh + lane] = obuf[q][lane];
+  } else {
+    if (hh == 0) wmax[wv][r] = m_run;
+    __syncthreads();  // also: every wave is past its last K-tile reads of its own tile
+    float m = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NS; ++w) m = fmaxf(m, wmax[w][r]);
+    const float sc = m_run == -INFINITY ? 0.f : expf(m_run - m);
+    if (hh == 0) wsum[wv][r] = l_run * sc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int d = (e & 3) + 8 * (e >> 2) + 4 * hh;
+      obuf[r][d] = o0[e] * sc;
+      obuf[r][d + 32] = o1[e] * sc;
+    }
+    __syncthreads();
+    // 32 x 64 outputs over 64 NS threads, partials summed in wave order
+    for (int i = threadIdx.x; i < 32 * kDh; i += 64 * NS) {
+      const int q = i / kDh, d = i % kDh;
+      if (q >= nrows) break;
+      float o = 0.f, l = 0.f;
+#pragma unroll
+      for (int w = 0; w < NS; ++w) {
+        o += reinterpret_cast<const float(*)[kDh + 1]>(tiles[w])[q][d];
+        l += wsum[w][q];
+      }
+      ctx[(row0 + q0 + q) * H + h * kDh + d] = l > 0.f ? o * (1.0f / l) : 0.f;
+    }
+  }
+}
+
+// K3 launch: one wave per (sequence, head, query tile) when those fill the chip, else NS
+// waves per triple splitting the key tiles (a 256-token single query: 96 waves -> 768).
+void launch_attention(int B, int L, int heads, int qt, int H, float scale, const float* qkv,
+                      const int* mask, float* ctx, hipStream_t s) {
+  const int triples = B * heads * qt, key_tiles = (L + 31) / 32;
+  const dim3 grid(triples);
+  if (key_tiles >= 8 && triples <= 256)
+    hipLaunchKernelGGL(attention_kernel<8>, grid, dim3(512), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
+  else if (key_tiles >= 4 && triples <= 512)
+    hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(256), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
+  else if (key_tiles >= 2 && triples <= 1024)
+    hipLaunchKernelGGL(attention_kernel<2>, grid, dim3(128), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
+  else
+    hipLaunchKernelGGL(attention_kernel<1>, grid, dim3(64), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
 }
 
 // K3 for the few-row forward (L <= 64 keys, one sequence's latency): one 512-thread
@@ -1575,8 +1654,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     }
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
-    hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L,
-                       H, c.heads, qt, scale, e->ctx.p);
+    launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
     // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y)
     gemm_resid_ln<VPL>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
                        w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
@@ -1787,8 +1865,7 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
         hipLaunchKernelGGL(attention_rows_kernel, dim3(B * c.heads * qt), dim3(512), 0, s, e->qkv.p, mask, L,
                            H, c.heads, qt, scale, e->ctx.p);
       else
-        hipLaunchKernelGGL(attention_kernel, dim3(B * c.heads * qt), dim3(64), 0, s, e->qkv.p, mask, L, H,
-                           c.heads, qt, scale, e->ctx.p);
+        launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
       e->tl.mark(s, ST_OPROJ);
       launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
     }

@@ -62,6 +62,27 @@ def test_shapes_vs_oracle(require_gpu, B, L, ragged, prec):
     _close(enc.embed(ids, mask), ref)
 
 
+@pytest.mark.parametrize("B,L,lens,kw", [
+    (1, 256, [256], {"pooling": POOL_MEAN}),          # 96 triples -> 8 waves per triple
+    (3, 200, [200, 3, 97], {"pooling": POOL_MEAN}),   # 8-way, whole key tiles fully masked
+    (6, 130, [130, 1, 64, 65, 100, 129], {}),         # 4 key tiles -> 4 waves per triple
+    (16, 96, [96] * 16, {"pooling": POOL_MEAN}),      # 576 triples -> 2 waves per triple
+    (1, 512, [300], {"gelu": GELU_TANH}),
+])
+def test_key_split_attention_vs_oracle(require_gpu, B, L, lens, kw):
+    """Few (sequence, head, query tile) triples with many keys (long single queries, the
+    CLS-only last layer) split the key tiles over 2 / 4 / 8 waves whose softmax partials
+    are merged in LDS (attention_kernel<NS>): against the oracle, ragged lengths."""
+    cfg = BertConfig(**{"layers": 2, **kw})
+    rng = np.random.default_rng(B * 7 + L)
+    ids = rng.integers(106, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.zeros((B, L), np.int32)
+    for b, n in enumerate(lens):
+        mask[b, :n] = 1
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    _close(Encoder(cfg).embed(ids, mask), ref)
+
+
 @pytest.mark.parametrize("B,L,kw", [
     (1, 32, {}), (1, 64, {}), (2, 32, {}), (3, 7, {}), (1, 1, {"layers": 1}),
     (1, 5, {"pooling": POOL_MEAN}), (2, 16, {"pooling": POOL_MEAN}), (1, 32, {"gelu": GELU_TANH}),

@@ -11,5 +11,5 @@ tail -1 gpurun_out/${TAG}_l32.json
 timeout -k 10 200 python -u tools/latency.py --iters 100 --encoder-seq-lens 16,32,48,64,96,128,256,512 > gpurun_out/${TAG}_lens.json 2>&1 || { echo LENS_FAIL; exit 1; }
 tail -1 gpurun_out/${TAG}_lens.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/tools/latency.py --iters 50 --encoder-seq-lens 32 > $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log 2>&1 || { echo PROF_FAIL; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/tools/latency.py --iters 50 --encoder-seq-lens ${PROF_LENS:-32} > $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log 2>&1 || { echo PROF_FAIL; exit 1; }
 echo ALL_OK
