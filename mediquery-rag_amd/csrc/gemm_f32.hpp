@@ -119,6 +119,32 @@ struct Stager {
   __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda, int M, int m0,
                                        const float* __restrict__ B, int64_t ldb, int64_t N,
                                        int64_t n0, int k0, int tid) {
+    if constexpr (T::A_SLOTS) {
+      // Buffer loads off two per-tile resources (scalar: the panel origins A + m0 lda and
+      // B + n0 ldb, so a corpus slab past 4 GB still takes 32-bit offsets), the slice's
+      // k0 in soffset, and a 32-bit per-slot offset (row clamped, 16-B chunk): 2 VALU per
+      // load instead of the 64-bit address arithmetic of a flat load (~60 VALU per slice).
+      const __amdgpu_buffer_rsrc_t ra =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)m0 * lda), (short)0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rb =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0 * ldb), (short)0, 0x7fffffff, 0x00020000);
+      const int alim = M - 1 - m0;                      // last valid row of the A panel
+      const int blim = (int)min(N - 1 - n0, (int64_t)T::BN - 1);
+      const int a4 = (int)lda * 4, b4 = (int)ldb * 4;
+#pragma unroll
+      for (int i = 0; i < T::LOADS; ++i) {
+        const int f = tid + i * T::THREADS;
+        if (T::PARTIAL && i == T::LOADS - 1 && f >= T::TOTAL_F4) break;
+        const int row = f / T::F4_PER_ROW, ch = f % T::F4_PER_ROW;
+        if (i < T::BM * T::F4_PER_ROW / T::THREADS)
+          r[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 ra, min(row, alim) * a4 + ch * 16, k0 * 4, 0));
+        else
+          r[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rb, min(row - T::BM, blim) * b4 + ch * 16, k0 * 4, 0));
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < T::LOADS; ++i) {
       const int f = tid + i * T::THREADS;
