@@ -103,7 +103,9 @@ int mq_index_get(mq_index* ix, int64_t row0, int64_t n, float* out, int out_on_d
  * approximate: recall vs exact is measured, not guaranteed).  dim % 64 == 0.
  * MQ_DTYPE_F32_SCREEN: exact fp32 results via certified screens (above): single queries
  * stream the bf16 shadow (half the HBM bytes), batches scan it on bf16 MFMA; scores are
- * the fp32 re-rank's dot products.  Synchronous (reads the certificate count back). */
+ * the fp32 re-rank's dot products.  Batches are asynchronous on `stream` (uncertified
+ * queries are re-run exactly on the device, mq_index_set_async_screen); single queries
+ * and the synchronous batch path read the certificate count back. */
 int mq_index_set_precision(mq_index* ix, int dtype);
 /* Batches of at most `max_queries` queries (default 4, 0..16; dim % 64 == 0, dim <= 1024)
  * use the streaming fp32 kernel instead of the MFMA tiles, whatever the precision. */
@@ -121,12 +123,21 @@ int mq_index_set_threshold_scan(mq_index* ix, int enabled);
  * run of failures (a corpus whose top scores crowd within the int8 bound) the int8 tier
  * sits out the next 256 searches.  0 = start at the bf16 stream tier.  Same results. */
 int mq_index_set_int8_screen(mq_index* ix, int enabled);
+/* Batched MQ_DTYPE_F32_SCREEN searches: 1 (default) = asynchronous - the certificate
+ * failures are never read back; two kernels enqueued after the certificate re-run the
+ * uncertified queries as an exact fp32 scan of every row (rerank arithmetic) and write
+ * their results in place, returning at once when nothing failed; once a failure has been
+ * seen (polled without waiting) the next 16 batches take the synchronous path.
+ * 0 = synchronous: read the failure count, re-run the failures one tier down (split-f32
+ * screen, then the direct exact scan).  Same results up to fp32 ties. */
+int mq_index_set_async_screen(mq_index* ix, int enabled);
 /* Counters of the k > 16 overflow checks so far (either pointer may be NULL): searches
  * re-scanned with 64-entry scan lists, and merges re-run with 64-entry thread lists. */
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
 /* Screen counters (MQ_DTYPE_F32_SCREEN; either pointer may be NULL): queries whose
- * certificates failed and that were re-run on the direct exact scan, and queries passed
- * down to the next screen (bf16 batch -> split-f32, int8 single -> bf16 stream). */
+ * certificates failed and that were re-run on the direct exact scan (or on the device
+ * by the asynchronous batch path: counting those synchronises the device), and queries
+ * passed down to the next screen (bf16 batch -> split-f32, int8 single -> bf16 stream). */
 int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
                                                          float* __restrict__ out, int ldo, int M,
                                                          int N, int K) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
   const int tiles_n = (N + T::BN - 1) / T::BN;
   const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
@@ -101,21 +101,31 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
     const int n0 = (int)n0l;
     if (m0 + T::BM <= M && n0 + T::BN <= N) {
       // full tile: every bias / residual load goes out before the first use, so the
-      // tile pays one memory round trip (the guarded loop below waits per element)
+      // tile pays one memory round trip (the guarded loop below waits per element).
+      // Residual loads and output stores are buffer ops off the wave tile's origin: one
+      // lane offset (column, lane half's row quad) in a VGPR, each register's row offset
+      // row(e) * ld a scalar soffset - no per-element address arithmetic.
+      const int wr0 = m0 + wm * T::WM, wc0 = n0 + wn * T::WN;
       float bv[T::TN];
 #pragma unroll
-      for (int tn = 0; tn < T::TN; ++tn) bv[tn] = bias[n0 + wn * T::WN + tn * 32 + (lane & 31)];
+      for (int tn = 0; tn < T::TN; ++tn) bv[tn] = bias[wc0 + tn * 32 + (lane & 31)];
       float rv[T::TM][T::TN][16];
       if constexpr (EPI == EPI_RESID) {
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(resid + (int64_t)wr0 * ldr + wc0), (short)0, 0x7fffffff, 0x00020000);
+        const int rl = (4 * (lane >> 5) * ldr + (lane & 31)) * 4;
 #pragma unroll
         for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
           for (int tn = 0; tn < T::TN; ++tn)
 #pragma unroll
             for (int e = 0; e < 16; ++e)
-              rv[tm][tn][e] = resid[(int64_t)(m0 + wm * T::WM + acc_row(tm, e, lane)) * ldr + n0 +
-                                    wn * T::WN + tn * 32 + (lane & 31)];
+              rv[tm][tn][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                  rr, rl, (acc_row(tm, e, 0) * ldr + tn * 32) * 4, 0));
       }
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(out + (int64_t)wr0 * ldo + wc0), (short)0, 0x7fffffff, 0x00020000);
+      const int ol = (4 * (lane >> 5) * ldo + (lane & 31)) * 4;
 #pragma unroll
       for (int tm = 0; tm < T::TM; ++tm)
 #pragma unroll
@@ -126,8 +136,7 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
             if (EPI == EPI_GELU_ERF) v = gelu_erf(v);
             if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
             if (EPI == EPI_RESID) v += rv[tm][tn][e];
-            out[(int64_t)(m0 + wm * T::WM + acc_row(tm, e, lane)) * ldo + n0 + wn * T::WN + tn * 32 +
-                (lane & 31)] = v;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ol, (acc_row(tm, e, 0) * ldo + tn * 32) * 4, 0);
           }
       return;
     }

@@ -818,12 +818,12 @@ __device__ __forceinline__ unsigned score_key(float x) {  // order-preserving, >
 }
 
 template <int KC, typename IdIn>
-__global__ __launch_bounds__(256) void merge_select_kernel(const float* __restrict__ cs,
-                                                           const IdIn* __restrict__ ci, int n_lists,
-                                                           int64_t nq, int k_in, int k_out,
-                                                           float* __restrict__ out_s,
-                                                           int64_t* __restrict__ out_i, int list_kc,
-                                                           int* __restrict__ overflow) {
+__device__ __forceinline__ void merge_select_block(const float* __restrict__ cs,
+                                                   const IdIn* __restrict__ ci, int n_lists,
+                                                   int64_t nq, int k_in, int k_out,
+                                                   float* __restrict__ out_s,
+                                                   int64_t* __restrict__ out_i, int list_kc,
+                                                   int* __restrict__ overflow, int64_t q) {
   constexpr int U = 8;
   __shared__ float ss[kSelCap];
   __shared__ long long si[kSelCap];
@@ -831,7 +831,6 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
   __shared__ int n_s;
   __shared__ float kth_s;
   __shared__ long long kth_i;
-  const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (n_lists > 256 * kSelHeads) {
     merge_threadlists<KC, IdIn>(cs, ci, n_lists, nq, k_in, k_out, out_s, out_i, list_kc, overflow, q);
@@ -939,6 +938,145 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
   }
 }
 
+template <int KC, typename IdIn>
+__global__ __launch_bounds__(256) void merge_select_kernel(const float* __restrict__ cs,
+                                                           const IdIn* __restrict__ ci, int n_lists,
+                                                           int64_t nq, int k_in, int k_out,
+                                                           float* __restrict__ out_s,
+                                                           int64_t* __restrict__ out_i, int list_kc,
+                                                           int* __restrict__ overflow) {
+  merge_select_block<KC, IdIn>(cs, ci, n_lists, nq, k_in, k_out, out_s, out_i, list_kc, overflow,
+                               blockIdx.x);
+}
+
+// ---------------------------------------------- asynchronous screen fallback ------
+// The batched certified screen (TIER_BF16) no longer reads its failure count back to the
+// host: these two kernels are enqueued after screen_verify_kernel every time and return
+// at once when *n_fail == 0.  Otherwise they compute, for each uncertified query fail[j],
+// the exact fp32 top-k over every row - the dot products in rerank_kernel's arithmetic
+// (lane-strided float4 fmaf chain + xor tree), so a fallback score is bitwise the score
+// the certified path reports for that (query, row) - and write it straight into the
+// caller's outputs.  Each workgroup scans a contiguous row range for up to kFbQ failed
+// queries per pass (one HBM pass per kFbQ queries); each wave keeps a top-k per query
+// in registers (lane i < k holds entry i, sorted by (score desc, id asc)), the 4 wave
+// lists are ranked in LDS into the workgroup's sorted list [g][nq][k], and
+// fallback_merge_kernel merges the G lists per query (merge_select_block).
+constexpr int kFbQ = 4;
+
+__device__ __forceinline__ void fb_insert(float& ls, int& li, int& cnt, float& ws, int& wi, float s,
+                                          int id, int k, int lane) {
+  if (cnt == k && !better(s, id, ws, wi)) return;  // wave-uniform
+  const int p = __popcll(__ballot(lane < cnt && better(ls, li, s, id)));
+  const float us = __shfl_up(ls, 1);
+  const int ui = __shfl_up(li, 1);
+  if (lane == p) {
+    ls = s;
+    li = id;
+  } else if (lane > p && lane < k) {
+    ls = us;
+    li = ui;
+  }
+  cnt = min(cnt + 1, k);
+  ws = __shfl(ls, k - 1);
+  wi = __shfl(li, k - 1);
+}
+
+__global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ Q,
+                                                            const float* __restrict__ rows, int dim,
+                                                            int64_t n, const int* __restrict__ n_fail,
+                                                            const int64_t* __restrict__ fail, int k,
+                                                            int64_t nq_cap, float* __restrict__ cs,
+                                                            int64_t* __restrict__ ci) {
+  const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
+  if (nf == 0) return;
+  __shared__ float ws_l[4 * MQ_MAX_K];
+  __shared__ int wi_l[4 * MQ_MAX_K];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t G = gridDim.x;
+  const int r0 = (int)(n * blockIdx.x / G), r1 = (int)(n * (blockIdx.x + 1) / G);
+  const int d4 = dim / 4;
+  for (int j0 = 0; j0 < nf; j0 += kFbQ) {
+    const floatx4* q4[kFbQ];
+#pragma unroll
+    for (int u = 0; u < kFbQ; ++u)
+      q4[u] = reinterpret_cast<const floatx4*>(Q + fail[min(j0 + u, nf - 1)] * (int64_t)dim);
+    float ls[kFbQ], wsc[kFbQ];
+    int li[kFbQ], cnt[kFbQ], wid[kFbQ];
+#pragma unroll
+    for (int u = 0; u < kFbQ; ++u) {
+      ls[u] = -INFINITY;
+      li[u] = -1;
+      cnt[u] = 0;
+      wsc[u] = -INFINITY;
+      wid[u] = -1;
+    }
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const floatx4* c4 = reinterpret_cast<const floatx4*>(rows + (int64_t)r * dim);
+      float acc[kFbQ];
+#pragma unroll
+      for (int u = 0; u < kFbQ; ++u) acc[u] = 0.f;
+      for (int i = lane; i < d4; i += 64) {
+        const floatx4 b = c4[i];
+#pragma unroll
+        for (int u = 0; u < kFbQ; ++u) {
+          const floatx4 a = q4[u][i];
+          acc[u] = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc[u]))));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kFbQ; ++u) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
+        fb_insert(ls[u], li[u], cnt[u], wsc[u], wid[u], acc[u], r, k, lane);
+      }
+    }
+    // rank the 4 wave lists of each query into the workgroup's sorted list (padding
+    // (-inf, -1) entries tie: the LDS position breaks the tie so every slot is written)
+#pragma unroll
+    for (int u = 0; u < kFbQ; ++u) {
+      if (j0 + u >= nf) break;  // block-uniform
+      if (lane < k) {
+        ws_l[wave * k + lane] = ls[u];
+        wi_l[wave * k + lane] = li[u];
+      }
+      __syncthreads();
+      if (tid < 4 * k) {
+        const float x = ws_l[tid];
+        const int xi = wi_l[tid];
+        int rank = 0;
+        for (int v = 0; v < 4 * k; ++v)
+          rank += (better(ws_l[v], wi_l[v], x, xi) || (ws_l[v] == x && wi_l[v] == xi && v < tid)) ? 1 : 0;
+        if (rank < k) {
+          const int64_t o = ((int64_t)blockIdx.x * nq_cap + j0 + u) * k + rank;
+          cs[o] = x;
+          ci[o] = xi;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// One block per possible failure slot j (grid = the batch size): blocks j >= *n_fail
+// return; block j merges the G workgroup lists of fail[j] into the outputs' row fail[j].
+// Block 0 adds the count to the index's cumulative fallback counter.
+template <int KC>
+__global__ __launch_bounds__(256) void fallback_merge_kernel(const float* __restrict__ cs,
+                                                             const int64_t* __restrict__ ci, int G,
+                                                             int64_t nq_cap, int k,
+                                                             const int* __restrict__ n_fail,
+                                                             const int64_t* __restrict__ fail,
+                                                             float* __restrict__ os,
+                                                             int64_t* __restrict__ oi,
+                                                             unsigned long long* __restrict__ total) {
+  const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
+  const int64_t j = blockIdx.x;
+  if (j == 0 && threadIdx.x == 0 && nf > 0) atomicAdd(total, (unsigned long long)nf);
+  if (j >= nf) return;
+  const int64_t shift = (fail[j] - j) * k;  // the block writes row j of (os + shift) = row fail[j]
+  merge_select_block<KC, int64_t>(cs, ci, G, nq_cap, k, k, os + shift, oi + shift, k, nullptr, j);
+}
+
 }  // namespace mq
 
 // ================================================================ host side =====
@@ -1009,6 +1147,16 @@ struct mq_index {
   bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
   double i8_fail_avg = 0.0;      // running share of single queries the int8 screen failed to certify
   int i8_skip = 0;               // searches left that bypass the int8 tier after a bad run
+  // asynchronous batched screen (TIER_BF16): the uncertified queries are re-run on the
+  // device (fallback_scan / fallback_merge) instead of behind a host read of the failure
+  // count; after a batch is seen to have failed, the next kAsyncCooldown batched screens
+  // run the synchronous tiered path (split-f32 tier first, cheaper for many failures)
+  bool async_screen = true;
+  int sync_left = 0;
+  DevBuf afb_cs, afb_ci, afb_total;  // fallback lists [G][nq][k]; cumulative count (u64)
+  unsigned long long* afb_host = nullptr;  // pinned copy of the cumulative count
+  hipEvent_t afb_event = nullptr;          // recorded after that copy
+  unsigned long long afb_seen = 0;         // count already folded into screen_fallbacks
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -1442,6 +1590,62 @@ bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
   return nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024;
 }
 
+constexpr int kAsyncCooldown = 16;
+
+// Fold a completed pinned copy of the device fallback count into screen_fallbacks (no
+// wait: an unfinished copy is read at a later call); a new failure starts the cooldown.
+void poll_async_fallbacks(mq_index* ix) {
+  if (!ix->afb_event || hipEventQuery(ix->afb_event) != hipSuccess) return;
+  const unsigned long long tot = *ix->afb_host;
+  if (tot > ix->afb_seen) {
+    ix->screen_fallbacks += (int64_t)(tot - ix->afb_seen);
+    ix->afb_seen = tot;
+    ix->sync_left = kAsyncCooldown;
+  }
+}
+
+// Device-side exact re-run of the uncertified queries (count and list from
+// screen_verify_kernel), results written into os / oi; nothing is read back.
+int launch_async_fallback(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
+                          const int64_t* fail, hipStream_t s) {
+  const int G = ix->num_cus;
+  int rc = ix->afb_cs.ensure((size_t)G * nq * k * sizeof(float));
+  if (!rc) rc = ix->afb_ci.ensure((size_t)G * nq * k * sizeof(int64_t));
+  if (!rc && !ix->afb_total.p) {
+    rc = ix->afb_total.ensure(sizeof(unsigned long long));
+    if (!rc) MQ_HIP(hipMemset(ix->afb_total.p, 0, sizeof(unsigned long long)));
+  }
+  if (rc) return rc;
+  if (!ix->afb_host) {
+    MQ_HIP(hipHostMalloc((void**)&ix->afb_host, sizeof(unsigned long long), hipHostMallocDefault));
+    *ix->afb_host = 0;
+  }
+  if (!ix->afb_event) MQ_HIP(hipEventCreateWithFlags(&ix->afb_event, hipEventDisableTiming));
+  const int* nf = ix->flag.as<int>();
+  hipLaunchKernelGGL(fallback_scan_kernel, dim3(G), dim3(256), 0, s, q, ix->rows, ix->dim, ix->n, nf, fail, k,
+                     nq, ix->afb_cs.as<float>(), ix->afb_ci.as<int64_t>());
+  auto* tot = ix->afb_total.as<unsigned long long>();
+  const dim3 grid((unsigned)nq);
+  switch (kc_merge(k)) {
+    case 8:
+      hipLaunchKernelGGL(fallback_merge_kernel<8>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
+                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
+      break;
+    case 16:
+      hipLaunchKernelGGL(fallback_merge_kernel<16>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
+                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
+      break;
+    default:
+      hipLaunchKernelGGL(fallback_merge_kernel<64>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
+                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
+      break;
+  }
+  MQ_HIP(hipGetLastError());
+  MQ_HIP(hipMemcpyAsync(ix->afb_host, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipEventRecord(ix->afb_event, s));
+  return MQ_OK;
+}
+
 int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, float* os,
                     int64_t* oi, hipStream_t s) {
   const bool bf = tier == TIER_BF16_STREAM || tier == TIER_BF16;
@@ -1492,6 +1696,11 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
                        ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
                        fail);
     MQ_HIP(hipGetLastError());
+    if (tier == TIER_BF16) {
+      poll_async_fallbacks(ix);
+      if (ix->async_screen && ix->sync_left == 0) return launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
+      if (ix->sync_left > 0) --ix->sync_left;
+    }
   }
   int n_fail = 0;
   rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);
@@ -1633,6 +1842,11 @@ int mq_index_destroy(mq_index* ix) {
     for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->rows8,
                       &ix->scale8, &ix->stats8})
       b->release();
+    ix->afb_cs.release();
+    ix->afb_ci.release();
+    ix->afb_total.release();
+    if (ix->afb_host) (void)hipHostFree(ix->afb_host);
+    if (ix->afb_event) (void)hipEventDestroy(ix->afb_event);
     for (int t = 0; t < 4; ++t) {
       ix->tier_fail[t].release();
       ix->tier_q[t].release();
@@ -1864,8 +2078,25 @@ int mq_index_set_int8_screen(mq_index* ix, int enabled) {
 int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split) {
   clear_error();
   MQ_CHECK_ARG(ix, "NULL argument");
-  if (to_direct) *to_direct = ix->screen_fallbacks;
+  int64_t pending = 0;  // asynchronous re-runs not yet folded in: read the device count
+  if (ix->afb_total.p) {
+    DeviceGuard dg(ix->device);
+    MQ_HIP(hipDeviceSynchronize());
+    unsigned long long tot = 0;
+    MQ_HIP(hipMemcpy(&tot, ix->afb_total.p, sizeof(tot), hipMemcpyDeviceToHost));
+    pending = (int64_t)(tot - ix->afb_seen);
+  }
+  if (to_direct) *to_direct = ix->screen_fallbacks + pending;
   if (to_split) *to_split = ix->screen_passdowns;
+  return MQ_OK;
+}
+
+int mq_index_set_async_screen(mq_index* ix, int enabled) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->async_screen = enabled != 0;
+  ix->sync_left = 0;
   return MQ_OK;
 }
 

@@ -69,6 +69,7 @@ SIGNATURES = {
     "mq_index_set_stream_threshold": (_I, [_P, _I]),
     "mq_index_set_threshold_scan": (_I, [_P, _I]),
     "mq_index_set_int8_screen": (_I, [_P, _I]),
+    "mq_index_set_async_screen": (_I, [_P, _I]),
     "mq_index_rescans": (_I, [_P, _P, _P]),
     "mq_index_screen_fallbacks": (_I, [_P, _P, _P]),
     "mq_index_set_timing": (_I, [_P, _I]),
@@ -109,7 +110,12 @@ def lib():
             raise ImportError("libmqhip.so not found at %s - build it with "
                               "`make -C mediquery-rag_amd/csrc` or __graft_entry__.build()" % LIB_PATH)
         h = ctypes.CDLL(LIB_PATH)
+        # A/B runs of an older build (tools/ab_*.sh) may lack symbols added since: only
+        # then (MQ_LIB_ALLOW_MISSING=1) are absent entry points left unbound
+        allow_missing = os.environ.get("MQ_LIB_ALLOW_MISSING") == "1"
         for name, (res, args) in SIGNATURES.items():
+            if allow_missing and not hasattr(h, name):
+                continue
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

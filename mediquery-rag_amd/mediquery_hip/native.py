@@ -102,6 +102,11 @@ class FlatIndex:
         straight to the bf16 stream tier.  Same results either way."""
         _lib.call("mq_index_set_int8_screen", self._h, int(bool(enabled)))
 
+    def set_async_screen(self, enabled=True):
+        """Batched screened searches: uncertified queries re-run exactly on the device with
+        no host read-back (default), or the synchronous tiered re-run.  Same results."""
+        _lib.call("mq_index_set_async_screen", self._h, int(bool(enabled)))
+
     @property
     def rescans(self):
         """Searches whose k > 16 list-overflow check fired (re-scanned with 64 lists)."""

@@ -349,6 +349,54 @@ def test_screened_falls_back_when_uncertified(require_gpu):
     assert i1[0].tolist() == [1000, 1001, 1002, 1003, 1004]
 
 
+def _dup_corpus(n_fail, n=6000, copies=70, seed=0):
+    """Queries 0..n_fail-1 each get `copies` exact duplicate rows (ids 1000 + 80 j ..):
+    their top scores tie beyond the 64 screen candidates, so no certificate can hold."""
+    c = synth.corpus(n, 768, seed=seed, clustered=True)
+    q, _ = synth.queries(128, c, seed=seed)
+    for j in range(n_fail):
+        c[1000 + 80 * j:1000 + 80 * j + copies] = q[j]
+    return c, q
+
+
+@pytest.mark.parametrize("n_fail,k", [(1, 5), (6, 5), (9, 50), (5, 16)])
+def test_async_screen_fallback_exact(require_gpu, n_fail, k):
+    """The default batched screen never reads its certificate back: uncertified queries
+    are re-run on the device (fallback_scan / fallback_merge, several queries per row
+    pass, k up to 64) and written in place.  Results equal the oracle, the duplicates come
+    out in id order, the count reaches screen_fallbacks, and after a failure has been
+    observed the next batches take the synchronous tiered path (same results)."""
+    c, q = _dup_corpus(n_fail)
+    ref = exact_scores(q, c)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, k)
+    assert check_topk(i, s, ref, k) == []
+    for j in range(n_fail):
+        assert i[j].tolist() == list(range(1000 + 80 * j, 1000 + 80 * j + k)), j
+    # (at k = 50 over 6000 rows other queries' 50th and 64th scores crowd within the
+    # bf16 bound too: they fail and are re-run the same way)
+    assert ix.screen_fallbacks >= n_fail
+    s2, i2 = ix.search(q, k)  # failure seen -> synchronous tiers for the cooldown
+    assert check_topk(i2, s2, ref, k) == []
+    assert (i2 == i).all()
+    np.testing.assert_allclose(s2, s, atol=1e-6)
+    assert ix.screen_fallbacks + ix.screen_passdowns >= 2 * n_fail
+
+
+def test_async_screen_matches_sync_when_certified(require_gpu):
+    """No failures: the asynchronous and synchronous batched screens return bitwise the
+    same results (the fallback kernels exit at once)."""
+    c = synth.corpus(70000, 768, seed=4, clustered=True)
+    q, _ = synth.queries(200, c, seed=4)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    ix.set_async_screen(False)
+    s2, i2 = ix.search(q, 5)
+    assert (i == i2).all() and (s == s2).all()
+    assert ix.screen_fallbacks == 0
+    assert check_topk(i, s, exact_scores(q, c), 5) == []
+
+
 def _near_tie_rows(q, spacing, count, rng):
     """Rows at cosine 1 - m * spacing (m = 0..count-1) from unit query q."""
     out = []
@@ -374,6 +422,7 @@ def test_screened_passes_near_ties_to_split_f32(require_gpu):
         c[j * 70:(j + 1) * 70] = _near_tie_rows(q[j], 4e-5, 70, rng)
     q = q.astype(np.float32)
     ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    ix.set_async_screen(False)  # the tiered (synchronous) re-run
     s, i = ix.search(q, 5)
     assert ix.screen_passdowns >= 100
     assert ix.screen_fallbacks == 0
