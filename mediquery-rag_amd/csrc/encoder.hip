@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 constexpr int kDh = 64;
 
 template <int NS>
-__global__ __launch_bounds__(64 * NS) void attention_kernel(const float* __restrict__ qkv,
+__global__ __launch_bounds__(64 * NS, NS == 1 ? 3 : 1) void attention_kernel(const float* __restrict__ qkv,
                                                             const int* __restrict__ mask, int L,
                                                             int H, int heads, int q_tiles,
                                                             float scale, float* __restrict__ ctx) {
