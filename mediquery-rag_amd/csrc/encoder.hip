@@ -89,10 +89,12 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
   const int G = gridDim.x, per_xcd = G >> 3;
   const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
+  const FastDiv tnd(tiles_n);
   auto coords = [&](int i, int& m0, int64_t& n0) {
     const int t = i * G + xslot;
-    m0 = (t / tiles_n) * T::BM;
-    n0 = (int64_t)(t % tiles_n) * T::BN;
+    const int tr = tnd.div(t);
+    m0 = tr * T::BM;
+    n0 = (int64_t)(t - tr * tiles_n) * T::BN;
   };
   auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
     int m0;

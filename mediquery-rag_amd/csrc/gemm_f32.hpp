@@ -309,6 +309,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
+// Division by a launch-invariant divisor 1 <= d < 2^31 for dividends 0 <= n < 2^31 by a
+// magic multiplier (Granlund-Montgomery): q = (mulhi(n, m) + n) >> s, s = ceil(log2 d).
+// The tile walks divide slice and tile counters every K-slice; hipcc's signed 32-bit
+// division is ~25 scalar instructions (abs / mul_hi / sign fix-ups) - this is three.
+// (Checked exhaustively for d < 3000, n < 2000 and on random d, n < 2^31.)
+struct FastDiv {
+  unsigned d, m, s;
+  __device__ __forceinline__ explicit FastDiv(int d_) : d((unsigned)d_) {
+    s = d > 1 ? 32 - __builtin_clz(d - 1) : 0;
+    m = (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  }
+  __device__ __forceinline__ int div(int n) const {
+    return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> s);
+  }
+  __device__ __forceinline__ int mod(int n) const { return n - div(n) * (int)d; }
+};
+
 // Operands of a tile walk: A [M][lda], B [N][ldb], both K-contiguous, K % 32 == 0.
 struct TileOperands {
   const float* A;
@@ -337,8 +354,9 @@ __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOp
   const int nk = op.K / T::BK;
   const int S = n_tiles * nk;
   if (S == 0) return;
+  const FastDiv nkd(nk);
   auto fetch = [&](Stager<T>& st, int j) {
-    const int i = j / nk, kt = j - (j / nk) * nk;
+    const int i = nkd.div(j), kt = j - i * nk;
     int m0;
     int64_t n0;
     coords(i, m0, n0);
@@ -380,8 +398,8 @@ __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOp
       __builtin_amdgcn_sched_barrier(0);
       st[(d + 1) % D].store(lds + ((j + 1) & 1) * T::STAGE_FLOATS, tid);
       __syncthreads();
-      if ((j + 1) % nk == 0) {
-        epi(j / nk, acc, cur);
+      if (nkd.mod(j + 1) == 0) {
+        epi(nkd.div(j), acc, cur);
         zero_acc<T>(acc);
       }
     });
