@@ -1698,7 +1698,11 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     MQ_HIP(hipGetLastError());
     if (tier == TIER_BF16) {
       poll_async_fallbacks(ix);
-      if (ix->async_screen && ix->sync_left == 0) return launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
+      // (the fallback's per-workgroup lists take G nq k entries: very large batches stay
+      // on the synchronous path rather than reserve more than 256 MB for a rare event)
+      const bool fits = (size_t)ix->num_cus * nq * k * (sizeof(float) + sizeof(int64_t)) <= (256ull << 20);
+      if (ix->async_screen && ix->sync_left == 0 && fits)
+        return launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
       if (ix->sync_left > 0) --ix->sync_left;
     }
   }

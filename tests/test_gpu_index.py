@@ -383,6 +383,29 @@ def test_async_screen_fallback_exact(require_gpu, n_fail, k):
     assert ix.screen_fallbacks + ix.screen_passdowns >= 2 * n_fail
 
 
+def test_async_screen_fallback_many_failures_threshold_scan(require_gpu):
+    """130 of 256 queries uncertified on the threshold-scan path (>= 65536 rows): the device
+    fallback walks them 4 per row pass and every result equals the oracle; the
+    synchronous cooldown path then passes them down to the split-f32 tier (> 64 failures)
+    with the same ids."""
+    rng = np.random.default_rng(9)
+    c = synth.corpus(70000, 768, seed=9, clustered=True)
+    q, _ = synth.queries(256, c, seed=9)
+    fails = rng.choice(256, 130, replace=False)
+    for n, j in enumerate(fails):
+        c[200 * n:200 * n + 70] = q[j]
+    ref = exact_scores(q, c)
+    ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
+    s, i = ix.search(q, 5)
+    assert check_topk(i, s, ref, 5) == []
+    for n, j in enumerate(fails):
+        assert i[j].tolist() == list(range(200 * n, 200 * n + 5)), j
+    assert ix.screen_fallbacks >= 130
+    s2, i2 = ix.search(q, 5)
+    assert (i2 == i).all()
+    assert ix.screen_passdowns >= 130
+
+
 def test_async_screen_matches_sync_when_certified(require_gpu):
     """No failures: the asynchronous and synchronous batched screens return bitwise the
     same results (the fallback kernels exit at once)."""
