@@ -211,6 +211,9 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *                                projections (out-proj, FFN-down) on full-row tiles with
  *                                the LayerNorm in their epilogue (1) or GEMM + LayerNorm
  *                                launch (0, default: the full-row tiles measured slower)
+ *   MQ_ENC_OPT_SPLITK_TILES      tiled path, M <= 256 rows: a GEMM is split over K only when
+ *                                its direct grid has at most this many 32 x 128 tiles
+ *                                (0..4096, default 0 = one tile per CU)
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
@@ -218,6 +221,7 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 #define MQ_ENC_OPT_LN_ROWS_PER_WAVE 3
 #define MQ_ENC_OPT_FUSE_ATTN_OPROJ 4
 #define MQ_ENC_OPT_FUSED_LN 5
+#define MQ_ENC_OPT_SPLITK_TILES 6
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);

@@ -1460,11 +1460,12 @@ void launch_gemm_tile(const GemmArgs& g, int tile, int num_cus, hipStream_t s) {
 
 // Split-K factor for a GEMM that would under-fill the chip (0 = run it directly):
 // enough chunks for ~2 workgroups per CU, each chunk a multiple of 32 deep.
-int splitk_factor(const GemmArgs& g, int num_cus, int cap = 16) {
+int splitk_factor(const GemmArgs& g, int num_cus, int cap = 16, int tiles_max = 0) {
   if (!g.slab || g.N % 4 != 0) return 0;
   const int64_t tiles = (int64_t)((g.M + 31) / 32) * ((g.N + 127) / 128);  // 32 x 128 tiles
   const int64_t slots = 2 * (int64_t)num_cus;
-  if (tiles * 2 > slots || g.M > 256) return 0;
+  // split only grids of at most tiles_max direct tiles (0: one tile per CU)
+  if (tiles > (tiles_max > 0 ? tiles_max : num_cus) || g.M > 256) return 0;
   const int slices = g.K / kBK;
   // At most 16 chunks: deeper splits fill more CUs but the slab traffic and the ordered
   // reduction grow with S (single query, L=32: encoder p50 0.74 ms at 16 vs 0.88 ms at
@@ -1487,8 +1488,9 @@ void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
 }
 
 template <int EPI>
-void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false, int splitk_cap = 16) {
-  const int S = splitk_factor(g, num_cus, splitk_cap);
+void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false, int splitk_cap = 16,
+                 int splitk_tiles = 0) {
+  const int S = splitk_factor(g, num_cus, splitk_cap, splitk_tiles);
   if (S) {
     launch_splitk<EPI>(g, S, s);
     return;
@@ -1564,6 +1566,7 @@ struct mq_encoder {
   int rows_max = kRowsDefault;  // few-row forward up to this many token rows (0 = off)
   int rows_splits = 0;          // few-row FFN-down K splits (0 = automatic)
   int splitk_max = 16;          // deepest split-K of the tiled path's few-row GEMMs
+  int splitk_tiles = 0;         // split-K only grids of <= this many 32x128 tiles (0 = num_cus)
   int ln_rows_per_wave = 4;     // batched LayerNorm kernel: rows per wave
   bool fused_ln = false;        // batched residual GEMMs: LayerNorm in the epilogue (full-row tiles;
                                 // measured slower, kept as an option: DESIGN.md §4)
@@ -1579,7 +1582,7 @@ namespace {
 template <int EPI>
 void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6, e->splitk_max);
+  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6, e->splitk_max, e->splitk_tiles);
 }
 
 // Residual projection + LayerNorm: x = LN(A W^T + b + resid), through y (g.out) on the
@@ -1591,7 +1594,7 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
                    int stage, hipStream_t s) {
   const int H = VPL * 256;
   const unsigned rb = (unsigned)((g.M + 3) / 4);
-  const int S = splitk_factor(g, e->num_cus, e->splitk_max);
+  const int S = splitk_factor(g, e->num_cus, e->splitk_max, e->splitk_tiles);
   if constexpr (VPL <= 3) {  // (the 32 + H row image of hidden 1024 does not double-buffer in LDS)
     // full-row tiles with the LayerNorm in the epilogue: exact f32, unit-stride residual
     // rows written in place (the strided CLS-only layer's compact output would overwrite
@@ -2167,6 +2170,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value == 0 || value == 1, "fused_ln must be 0 or 1 (got %d)", value);
       e->fused_ln = value != 0;
       break;
+    case MQ_ENC_OPT_SPLITK_TILES:
+      MQ_CHECK_ARG(value >= 0 && value <= 4096, "splitk_tiles must be in [0, 4096] (got %d)", value);
+      e->splitk_tiles = value;
+      break;
     default:
       MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
@@ -2186,6 +2193,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_LN_ROWS_PER_WAVE: *value = e->ln_rows_per_wave; break;
     case MQ_ENC_OPT_FUSE_ATTN_OPROJ: *value = e->fuse_attn_oproj ? 1 : 0; break;
     case MQ_ENC_OPT_FUSED_LN: *value = e->fused_ln ? 1 : 0; break;
+    case MQ_ENC_OPT_SPLITK_TILES: *value = e->splitk_tiles; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
   return MQ_OK;

@@ -184,6 +184,7 @@ def test_errors(require_gpu):
     ("ln_rows_per_wave", 1, 9, 33), ("ln_rows_per_wave", 2, 9, 33),
     ("fuse_attn_oproj", 0, 1, 32), ("fuse_attn_oproj", 0, 2, 17),
     ("fused_ln", 1, 70, 32), ("fused_ln", 1, 9, 130),
+    ("splitk_tiles", 64, 1, 256), ("splitk_tiles", 4096, 1, 100), ("splitk_tiles", 16, 2, 48),
 ])
 def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     """Every non-default value of the explicit tuning options (mq_encoder_set_option,
@@ -196,12 +197,13 @@ def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     mask[-1, L // 2:] = 0
     ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
     enc = Encoder(cfg)
-    if name == "splitk_max":
+    if name in ("splitk_max", "splitk_tiles"):
         enc.set_option("rows_max", 0)
     if name == "ln_rows_per_wave":  # (the LayerNorm kernel runs on the unfused path)
         enc.set_option("fused_ln", 0)
     enc.set_option(name, value)
     assert enc.get_option(name) == value
     _close(enc.embed(ids, mask), ref)
-    with pytest.raises(_lib.MQError):
-        enc.set_option(name, 1000)
+    for bad in (-1, 1 << 20):
+        with pytest.raises(_lib.MQError):
+            enc.set_option(name, bad)

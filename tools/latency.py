@@ -51,17 +51,22 @@ def main():
                     help="comma list: only the single-query encoder p50 at these token counts")
     ap.add_argument("--rows-max", default="",
                     help="comma list of MQ_ENC_OPT_ROWS_MAX values to compare in --encoder-seq-lens mode")
+    ap.add_argument("--opt", default="",
+                    help="NAME=V1,V2,...: an encoder option (Encoder.OPTIONS) to sweep in --encoder-seq-lens mode")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.encoder_seq_lens:
         enc = Encoder(DMETA_BASE, device=0)
         q = torch.empty((1, 768), device=dev)
         res = {}
-        for rm in [int(x) for x in args.rows_max.split(",")] if args.rows_max else [None]:
+        name, vals = "rows_max", args.rows_max
+        if args.opt:
+            name, vals = args.opt.split("=")
+        for rm in [int(x) for x in vals.split(",")] if vals else [None]:
             tag = ""
             if rm is not None:
-                enc.set_option("rows_max", rm)
-                tag = "_rowsmax%d" % rm
+                enc.set_option(name, rm)
+                tag = "_%s%d" % (name.replace("_", ""), rm)
             for L in [int(x) for x in args.encoder_seq_lens.split(",")]:
                 ids_np, mask_np = synth.token_batch(1, L)
                 ids = torch.from_numpy(ids_np).to(dev)
