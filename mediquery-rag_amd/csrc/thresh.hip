@@ -419,14 +419,27 @@ __device__ __forceinline__ float key_ord(unsigned k) {
 #define MQ_I8_ROWS 8
 #endif
 constexpr int kI8Rows = MQ_I8_ROWS;  // rows per wave step (8 or 16)
-constexpr int kI8Stages = 2;  // register stages of the row stream (1 step in flight; a
-                              // third spills at dim 768 under the 3-workgroup budget)
+#ifndef MQ_I8_STAGES
+#define MQ_I8_STAGES 3
+#endif
+#ifndef MQ_I8_TAU_POP
+#define MQ_I8_TAU_POP 1  // in-kernel tau: per-lane top-k + wave pops (1) or bitwise ballot search (0)
+#endif
+constexpr int kI8Stages = MQ_I8_STAGES;  // register stages of the row stream (2 or 3: 3 measured
+                                         // 2-3 us faster per search, 158 VGPRs, no spills)
+static_assert(kI8Stages == 2 || kI8Stages == 3, "2 or 3 register stages");
 constexpr int kI8Lg = kI8Rows == 16 ? 4 : 3;
 static_assert(kI8Rows == 1 << kI8Lg, "8 or 16 rows per step");
 
 // values v[0 .. R NQ) indexed r * NQ + q -> lane l holds v[0 .. NQ) of row i8_row(l),
 // summed over the 64 lanes: log2 R halving exchanges (xor 32, 16, ...), then a plain
-// butterfly over the remaining lane bits
+// butterfly over the remaining lane bits.  A halving step pairs x = v[i] with
+// y = v[i + c/2]: lanes with bit m clear keep x and add their partner's x, the others
+// keep y and add their partner's y.  For m = 32 / 16 that is exactly one gfx950
+// v_permlane{32,16}_swap of (x, y) followed by x' + y' (no lane selects); for m = 8 / 4 a
+// select of the two values and one DPP row_ror:8 / swizzle xor-4 move.  Written as
+// `hi ? v[i + c/2] : v[i]` the compiler turned the selects into dynamically indexed
+// register chains (7 v_cmp + 7 v_cndmask per value, ~200 VALU per 8-row step).
 __device__ __forceinline__ int i8_row(int lane) {
   int r = 0;
 #pragma unroll
@@ -434,22 +447,49 @@ __device__ __forceinline__ int i8_row(int lane) {
   return r;
 }
 
+__device__ __forceinline__ float xor_move(float v, int m) {
+  const int b = __float_as_int(v);
+  switch (m) {
+    case 8: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x128, 0xf, 0xf, false));  // row_ror:8
+    case 4: return __int_as_float(__builtin_amdgcn_ds_swizzle(b, 0x101f));  // xor 4 (bit mode)
+    case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x4e, 0xf, 0xf, false));   // quad [2,3,0,1]
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
+    default: return __shfl_xor(v, m);
+  }
+}
+
+// max over the wave, every lane gets it: DPP / swizzle within 16 lanes, then the two swaps
+__device__ __forceinline__ unsigned wave_max_u32(unsigned m) {
+#pragma unroll
+  for (int off = 1; off <= 8; off <<= 1) m = max(m, (unsigned)__float_as_int(xor_move(__int_as_float((int)m), off)));
+  auto r = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+  m = max((unsigned)r[0], (unsigned)r[1]);
+  r = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  return max((unsigned)r[0], (unsigned)r[1]);
+}
+
 template <int NQ>
 __device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int lane) {
 #pragma unroll
   for (int m = 32, c = kI8Rows * NQ; m >= 64 / kI8Rows; m >>= 1, c >>= 1) {
-    const bool hi = (lane & m) != 0;
 #pragma unroll
     for (int i = 0; i < c / 2; ++i) {
-      const float keep = hi ? v[i + c / 2] : v[i];
-      const float give = hi ? v[i] : v[i + c / 2];
-      v[i] = keep + __shfl_xor(give, m);
+      const float x = v[i], y = v[i + c / 2];
+      if (m == 32 || m == 16) {
+        const auto r = m == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false)
+                               : __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      } else {
+        const bool hi = (lane & m) != 0;
+        const float keep = hi ? y : x, give = hi ? x : y;
+        v[i] = keep + xor_move(give, m);
+      }
     }
   }
 #pragma unroll
   for (int m = 32 / kI8Rows; m > 0; m >>= 1)
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) v[i] += __shfl_xor(v[i], m);
+    for (int i = 0; i < NQ; ++i) v[i] += xor_move(v[i], m);
 }
 
 template <int E4>
@@ -467,18 +507,31 @@ __device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t
 template <int E4, int NQ>
 __device__ __forceinline__ void i8_dot(const unsigned (&a)[kI8Rows][E4], const float (&qv)[NQ][4 * E4],
                                        float (&v)[kI8Rows * NQ]) {
+  // two rows per packed FMA (v_pk_fma_f32: one instruction for both rows' products,
+  // each row's chain in the same element order as a scalar fma chain)
+  typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int r = 0; r < kI8Rows; ++r) {
+  for (int r = 0; r < kI8Rows; r += 2) {
+    f2 acc[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) v[r * NQ + q] = 0.f;
+    for (int q = 0; q < NQ; ++q) acc[q] = f2{0.f, 0.f};
 #pragma unroll
     for (int d = 0; d < E4; ++d)
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const float x = (float)((int)(a[r][d] << (24 - 8 * b)) >> 24);  // signed byte b
+        const f2 x = {(float)((int)(a[r][d] << (24 - 8 * b)) >> 24),  // signed byte b
+                      (float)((int)(a[r + 1][d] << (24 - 8 * b)) >> 24)};
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) v[r * NQ + q] = fmaf(qv[q][4 * d + b], x, v[r * NQ + q]);
+        for (int q = 0; q < NQ; ++q) {
+          const f2 qq = {qv[q][4 * d + b], qv[q][4 * d + b]};
+          acc[q] = __builtin_elementwise_fma(qq, x, acc[q]);
+        }
       }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      v[r * NQ + q] = acc[q].x;
+      v[(r + 1) * NQ + q] = acc[q].y;
+    }
   }
 }
 
@@ -566,10 +619,42 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       }
   }
   if (u < n_units) fetch(0, u);
+  if (kI8Stages == 3 && u < n_units) fetch(1, u + stride);
   if (MODE == TS_APPEND) {
     if (tau_wave) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
+#if MQ_I8_TAU_POP
+        // the kTsRank-th largest key (with multiplicity): each lane keeps its own top
+        // kTsRank keys (compare-exchange insertion), then kTsRank rounds of a wave max
+        // whose lowest holder pops its head - ~450 VALU instead of 32 rounds of kPer ballots
+        // (~4k instructions while the workgroup's other waves wait at the barrier).  Same T.
+        unsigned top[kTsRank];
+#pragma unroll
+        for (int i = 0; i < kTsRank; ++i) top[i] = 0u;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          unsigned x = key[q][j];
+#pragma unroll
+          for (int i = 0; i < kTsRank; ++i) {
+            const unsigned hi = max(top[i], x);
+            x = min(top[i], x);
+            top[i] = hi;
+          }
+        }
+        unsigned T = 0;
+#pragma unroll
+        for (int r = 0; r < kTsRank; ++r) {
+          const unsigned m = wave_max_u32(top[0]);
+          T = m;
+          const unsigned long long holders = __ballot(top[0] == m);
+          if (r + 1 < kTsRank && lane == (int)__builtin_ctzll(holders)) {
+#pragma unroll
+            for (int i = 0; i + 1 < kTsRank; ++i) top[i] = top[i + 1];
+            top[kTsRank - 1] = 0u;
+          }
+        }
+#else
         unsigned T = 0;
         for (int b = 31; b >= 0; --b) {
           const unsigned cand = T | (1u << b);
@@ -578,6 +663,7 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
           for (int j = 0; j < kPer; ++j) c += __popcll(__ballot(key[q][j] >= cand));
           if (c >= kTsRank) T = cand;
         }
+#endif
         const float t = T == 0u ? -INFINITY : key_ord(T);
         if (lane == 0) {
           th_sh[q] = t;
@@ -589,16 +675,33 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
 #pragma unroll
     for (int q = 0; q < NQ; ++q) th[q] = th_sh[q];
   }
-  // two register stages: the next unit's loads are in flight while one is multiplied
-  while (u < n_units) {
-    const int64_t u1 = u + stride;
-    fetch(1, u1);
-    consume(0, u);
-    if (u1 >= n_units) break;
-    const int64_t u2 = u1 + stride;
-    fetch(0, u2);
-    consume(1, u1);
-    u = u2;
+  if constexpr (kI8Stages == 2) {
+    // two register stages: the next unit's loads are in flight while one is multiplied
+    while (u < n_units) {
+      const int64_t u1 = u + stride;
+      fetch(1, u1);
+      consume(0, u);
+      if (u1 >= n_units) break;
+      const int64_t u2 = u1 + stride;
+      fetch(0, u2);
+      consume(1, u1);
+      u = u2;
+    }
+  } else {
+    // three: the next two units' loads are in flight while one is multiplied (stage
+    // (i mod 3) holds unit u + i stride; fetch clamps past-the-end units to the last one)
+    constexpr int s2 = kI8Stages - 1;  // (2; the branch is only taken with three stages)
+    while (u < n_units) {
+      fetch(s2, u + 2 * stride);
+      consume(0, u);
+      if (u + stride >= n_units) break;
+      fetch(0, u + 3 * stride);
+      consume(1, u + stride);
+      if (u + 2 * stride >= n_units) break;
+      fetch(1, u + 4 * stride);
+      consume(s2, u + 2 * stride);
+      u += 3 * stride;
+    }
   }
   if (MODE == TS_MAX) {  // workgroup maxima: one list per workgroup (a shorter tau pass)
     __shared__ float wmax[4][NQ];
