@@ -3,7 +3,7 @@
 # latency, alternating in-tree / variants twice on the same box.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_i8.py tests/test_gpu_thresh.py tests/test_gpu_index.py -x -q --timeout 200 --timeout-method thread > gpurun_out/iv_tests_main.log 2>&1 || { echo TESTS_FAIL main; tail -30 gpurun_out/iv_tests_main.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_i8.py tests/test_gpu_thresh.py tests/test_gpu_index.py tests/test_gpu_store.py -x -q --timeout 200 --timeout-method thread > gpurun_out/iv_tests_main.log 2>&1 || { echo TESTS_FAIL main; tail -30 gpurun_out/iv_tests_main.log; exit 1; }
 echo main $(tail -1 gpurun_out/iv_tests_main.log)
 for v in variants/*.so; do
   n=$(basename $v .so)
