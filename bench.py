@@ -65,6 +65,8 @@ def parse():
                    help="also time the headline step at this L (0 = skip)")
     p.add_argument("--config4-steps", type=int, default=10,
                    help="BASELINE config 4 line (10M x 768 as 8 row shards, batch 1024): timed steps (0 = skip)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the config-2, clustered-corpus, long-query and k=50 extras")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     return p.parse_args()
@@ -207,6 +209,159 @@ def config4(args, enc, world, rank, dev, backend):
             "encoder_ms": round(statistics.mean(e[0].elapsed_time(e[1]) for e in evs), 3),
             "search_ms": round(statistics.mean(e[1].elapsed_time(e[2]) for e in evs), 3),
             "planted_top1_ok": ok, "screen_fallbacks": fb}
+
+
+def _timed_steps(fn, steps, warmup):
+    """Wall time of `steps` calls of fn after `warmup` (device synchronised both sides)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _counters(ix):
+    return {"batch_fallbacks": ix.screen_fallbacks, "passdowns": ix.screen_passdowns,
+            "bf16_tier_skips": ix.screen_skips, "int8_tier_skips": ix.int8_skips}
+
+
+def config2(args, enc, dev, ids, mask, q):
+    """BASELINE config 2: 100k x 768 fp32 corpus, batch 256 (L = 32) embed + exact top-k
+    on one GPU, timed like the headline (exact fp32 via the certified screen)."""
+    n = 100_000
+    ix = FlatIndex(dim=768, capacity=n, device=dev.index)
+    ix.add_device(synth.corpus_device(n, 768, dev, seed=synth.CORPUS_SEED + 2))
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    B, K = q.shape[0], args.k
+    s = torch.empty((B, K), dtype=torch.float32, device=dev)
+    i = torch.empty((B, K), dtype=torch.int64, device=dev)
+
+    def step():
+        enc.embed_device(ids, mask, q)
+        ix.search_device(q, K, s, i)
+
+    t = _timed_steps(step, args.steps, args.warmup)
+    t_s = _timed_steps(lambda: ix.search_device(q, K, s, i), args.steps, 2)
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    s2, i2 = torch.empty_like(s), torch.empty_like(i)
+    ix.search_device(q, K, s2, i2)
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    ix.search_device(q, K, s, i)
+    torch.cuda.synchronize()
+    out = {"workload": "BASELINE config 2: %d x 768 fp32 corpus, batch %d (L=%d) embed + exact top-%d" % (n, B, args.seq_len, K),
+           "queries_per_s": round(B / t, 1), "ms_per_step": round(t * 1e3, 3), "steps": args.steps,
+           "search_ms": round(t_s * 1e3, 4),
+           "ids_equal_direct_exact": bool((i == i2).all()), "counters": _counters(ix)}
+    ix.close()
+    return out
+
+
+def exact_k50(index, q, dev):
+    """The exact top-50 batch (screened) beside the direct exact scan: the large-k path
+    that skips the bf16 tier (r3 paid a 157 ms device fallback here)."""
+    B, k = q.shape[0], 50
+    s = torch.empty((B, k), dtype=torch.float32, device=dev)
+    i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    s2, i2 = torch.empty_like(s), torch.empty_like(i)
+    c0 = _counters(index)
+    index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    t_scr = _timed_steps(lambda: index.search_device(q, k, s, i), 10, 2)
+    index.set_precision(_lib.MQ_DTYPE_F32)
+    t_dir = _timed_steps(lambda: index.search_device(q, k, s2, i2), 10, 2)
+    index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    c1 = _counters(index)
+    return {"batch": B, "k": k, "screened_ms": round(t_scr * 1e3, 3), "direct_ms": round(t_dir * 1e3, 3),
+            "ratio": round(t_scr / t_dir, 3), "ids_equal_frac": round(float((i == i2).float().mean()), 6),
+            "counters": {kk: c1[kk] - c0[kk] for kk in c1}}
+
+
+def long_queries(args, enc, index, dev, K):
+    """Single-query p50 (embed + screened search) at the advisor path's query lengths
+    (200-500 chars, src/ui/interface.py:437-479): L = 128 / 256 / 512 tokens."""
+    out = {}
+    s = torch.empty((1, K), dtype=torch.float32, device=dev)
+    i = torch.empty((1, K), dtype=torch.int64, device=dev)
+    q1 = torch.empty((1, 768), dtype=torch.float32, device=dev)
+    for L in (128, 256, 512):
+        ids_np, mask_np = synth.token_batch(1, L, seed=synth.TOKEN_SEED + L)
+        ids1, mask1 = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
+        lat, enc_l = [], []
+        for it in range(35):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            enc.embed_device(ids1, mask1, q1)
+            torch.cuda.synchronize()
+            b = time.perf_counter()
+            index.search_device(q1, K, s, i)
+            torch.cuda.synchronize()
+            if it >= 5:
+                lat.append((time.perf_counter() - a) * 1e3)
+                enc_l.append((b - a) * 1e3)
+        out["L%d" % L] = {"p50_ms": round(statistics.median(lat), 3),
+                          "encoder_p50_ms": round(statistics.median(enc_l), 3)}
+    return out
+
+
+def clustered(args, enc, dev, ids, mask, q):
+    """The headline step where the certificate is stressed (SURVEY.md §8d clustered
+    variant: 4096 centroids, sigma 0.35, the reference corpus's duplicate-row pattern):
+    (a) the config-3 step (encoder queries), (b) search-only batches of in-distribution
+    queries (each a corpus row + noise: its cluster-mates crowd the top scores), (c)
+    single in-distribution queries; certificate counters for each, and the direct exact
+    scan beside (b) for ids and time."""
+    n = args.corpus_rows
+    rows, _ = synth.clustered_corpus_device(n, 768, dev)
+    ix = FlatIndex(dim=768, capacity=n, device=dev.index)
+    ix.add_device(rows)
+    B, K = q.shape[0], args.k
+    pq, _ = synth.queries_device(B, rows, seed=synth.QUERY_SEED + 11, planted_frac=1.0)
+    del rows
+    torch.cuda.empty_cache()
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    s = torch.empty((B, K), dtype=torch.float32, device=dev)
+    i = torch.empty((B, K), dtype=torch.int64, device=dev)
+
+    def step():
+        enc.embed_device(ids, mask, q)
+        ix.search_device(q, K, s, i)
+
+    c0 = _counters(ix)
+    t_step = _timed_steps(step, args.steps, args.warmup)
+    c1 = _counters(ix)
+    t_pq = _timed_steps(lambda: ix.search_device(pq, K, s, i), args.steps, 2)
+    c2 = _counters(ix)
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    s2, i2 = torch.empty_like(s), torch.empty_like(i)
+    t_dir = _timed_steps(lambda: ix.search_device(pq, K, s2, i2), args.steps, 2)
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    ix.search_device(pq, K, s, i)
+    torch.cuda.synchronize()
+    same = float((i == i2).float().mean())
+    lat = []
+    s1, i1 = s[:1], i[:1]
+    c3 = _counters(ix)
+    for j in range(min(B, 100)):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        ix.search_device(pq[j:j + 1], K, s1, i1)
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - a) * 1e3)
+    c4 = _counters(ix)
+    d = lambda x, y: {kk: y[kk] - x[kk] for kk in y}
+    ix.close()
+    return {"workload": "%d x 768 clustered corpus (4096 centroids, sigma 0.35, reference duplicate-row "
+                        "pattern), batch %d, k=%d" % (n, B, K),
+            "step_queries_per_s": round(B / t_step, 1), "step_ms": round(t_step * 1e3, 3),
+            "step_counters": d(c0, c1),
+            "in_distribution_search_ms": round(t_pq * 1e3, 4),
+            "in_distribution_direct_search_ms": round(t_dir * 1e3, 4),
+            "in_distribution_ids_equal_direct": round(same, 6),
+            "in_distribution_counters": d(c1, c2),
+            "single_query_search_p50_ms": round(statistics.median(lat), 4),
+            "single_query_counters": d(c3, c4)}
 
 
 def workload_name(rows, batch, world):
@@ -434,6 +589,14 @@ def main():
 
     c4 = config4(args, enc, world, rank, dev, backend) if args.config4_steps > 0 else None
 
+    extras = {}
+    if world == 1 and not args.no_extras:
+        extras["exact_k50_batch"] = exact_k50(index, q, dev)
+        extras["long_query_p50"] = long_queries(args, enc, index, dev, K)
+        extras["config2"] = config2(args, enc, dev, ids, mask, q)
+        extras["clustered_corpus"] = clustered(args, enc, dev, ids, mask, q)
+    run_counters = _counters(index)  # every search of the run, timed or not
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -544,6 +707,8 @@ def main():
     out["config4_sharded"] = c4
     out["config5_bf16_rerank"] = cfg5
     out["secondary_long_queries"] = sec
+    out["screen_counters_whole_run"] = run_counters
+    out.update(extras)
     if world == 1 and not args.no_cpu_baseline:
         def corpus_host():
             return torch.nn.functional.normalize(

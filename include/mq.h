@@ -124,10 +124,15 @@ int mq_index_set_threshold_scan(mq_index* ix, int enabled);
  * sits out the next 256 searches.  0 = start at the bf16 stream tier.  Same results. */
 int mq_index_set_int8_screen(mq_index* ix, int enabled);
 /* Batched MQ_DTYPE_F32_SCREEN searches: 1 (default) = asynchronous - the certificate
- * failures are never read back; two kernels enqueued after the certificate re-run the
- * uncertified queries as an exact fp32 scan of every row (rerank arithmetic) and write
- * their results in place, returning at once when nothing failed; once a failure has been
- * seen (polled without waiting) the next 16 batches take the synchronous path.
+ * failures are never read back; kernels enqueued after the certificate gather the
+ * uncertified queries and re-run ALL of them in one exact-f32 MFMA pass over the slab
+ * (the direct scan's tile, shape picked on the device from the failure count), merge
+ * and write their results in place, returning at once when nothing failed; once a
+ * failure has been seen (polled without waiting) the next 16 batches take the
+ * synchronous path, and a failure share above 0.2 there sends the next 64 batches
+ * straight to the split-f32 screen.
+ * The bf16 tier serves k <= 16 only (its 64 candidates leave no margin past that): larger
+ * k runs the split-f32 screen (batches > 64) or the direct exact scan.
  * 0 = synchronous: read the failure count, re-run the failures one tier down (split-f32
  * screen, then the direct exact scan).  Same results up to fp32 ties. */
 int mq_index_set_async_screen(mq_index* ix, int enabled);
@@ -136,9 +141,15 @@ int mq_index_set_async_screen(mq_index* ix, int enabled);
 int mq_index_rescans(const mq_index* ix, int64_t* rescans, int64_t* remerges);
 /* Screen counters (MQ_DTYPE_F32_SCREEN; either pointer may be NULL): queries whose
  * certificates failed and that were re-run on the direct exact scan (or on the device
- * by the asynchronous batch path: counting those synchronises the device), and queries
- * passed down to the next screen (bf16 batch -> split-f32, int8 single -> bf16 stream). */
+ * by the asynchronous batch path: counting those waits for the last asynchronous
+ * search's count copy on its stream), and queries passed down to the next screen
+ * (bf16 batch -> split-f32, int8 single -> bf16 stream). */
 int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split);
+/* Screened searches that bypassed a tier after a run of failed certificates (either
+ * pointer may be NULL): batches that skipped the bf16 tier (failure share above 0.2: it
+ * sits out 64 searches, then is tried again), and single queries that skipped the int8
+ * tier (share above 0.3: it sits out 256). */
+int mq_index_screen_skips(const mq_index* ix, int64_t* bf16_skips, int64_t* int8_skips);
 /* Device pointer of the row slab ([capacity, dim] of the index dtype). */
 int mq_index_data(mq_index* ix, void** device_rows);
 /* Device-time accounting with HIP events on the launch stream (off by default).

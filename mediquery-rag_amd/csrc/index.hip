@@ -93,10 +93,30 @@ struct SearchSmem {
 // Scores never leave the chip: each finished tile goes accumulator -> LDS (the stage
 // buffer the last slice released) -> one lane per (query, part) scans its row against
 // its register top-KC list; only beating the list tail costs an insertion.
+// Scan geometry shared by the host plan and the device-count fallback (which picks it
+// in-kernel from the failure count): nqt query tiles of BM, G row groups (a multiple of
+// 8, <= the row tiles) so that about per_cu x CUs workgroups run.
+struct ScanGeom {
+  int nqt, G;
+};
+__host__ __device__ inline ScanGeom scan_geom(int64_t nq, int BM, int BN, int per_cu, int num_cus,
+                                              int64_t n_rows) {
+  ScanGeom g;
+  g.nqt = (int)((nq + BM - 1) / BM);
+  const int64_t ntiles = (n_rows + BN - 1) / BN;
+  int64_t G = (int64_t)per_cu * num_cus / g.nqt;
+  G = G < 1 ? 1 : G;
+  G = G > ntiles ? ntiles : G;
+  g.G = (int)((G + 7) / 8 * 8);
+  return g;
+}
+
 template <class T, int KC>
-__global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
-    const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
-    int G, int nqt, int kl, float* __restrict__ cand_s, int* __restrict__ cand_i) {
+__device__ __forceinline__ void flat_search_block(const float* __restrict__ Q, int nq,
+                                                  const float* __restrict__ C, int64_t n_rows,
+                                                  int dim, int G, int nqt, int kl,
+                                                  float* __restrict__ cand_s,
+                                                  int* __restrict__ cand_i, int b) {
   using S = SearchSmem<T>;
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
 
@@ -105,7 +125,7 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
 
   // blocks b and b+8 share an XCD: give the nqt query tiles of one row group to one
   // XCD so the second read of each row tile is an L2 hit.
-  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int xcd = b & 7, slot = b >> 3;
   const int qt = slot % nqt, g = (slot / nqt) * 8 + xcd;
   const int m0 = qt * T::BM;
   const int64_t ntiles = (n_rows + T::BN - 1) / T::BN;
@@ -163,6 +183,13 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
         cand_i[base + i] = top.id[i];
       }
   }
+}
+
+template <class T, int KC>
+__global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
+    const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
+    int G, int nqt, int kl, float* __restrict__ cand_s, int* __restrict__ cand_i) {
+  flat_search_block<T, KC>(Q, nq, C, n_rows, dim, G, nqt, kl, cand_s, cand_i, blockIdx.x);
 }
 
 // ============================================ K9s: streaming scan, few queries ==
@@ -950,120 +977,52 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
 }
 
 // ---------------------------------------------- asynchronous screen fallback ------
-// The batched certified screen (TIER_BF16) no longer reads its failure count back to the
-// host: these two kernels are enqueued after screen_verify_kernel every time and return
-// at once when *n_fail == 0.  Otherwise they compute, for each uncertified query fail[j],
-// the exact fp32 top-k over every row - the dot products in rerank_kernel's arithmetic
-// (lane-strided float4 fmaf chain + xor tree), so a fallback score is bitwise the score
-// the certified path reports for that (query, row) - and write it straight into the
-// caller's outputs.  Each workgroup scans a contiguous row range for up to kFbQ failed
-// queries per pass (one HBM pass per kFbQ queries); each wave keeps a top-k per query
-// in registers (lane i < k holds entry i, sorted by (score desc, id asc)), the 4 wave
-// lists are ranked in LDS into the workgroup's sorted list [g][nq][k], and
-// fallback_merge_kernel merges the G lists per query (merge_select_block).
-constexpr int kFbQ = 4;
+// The batched certified screen (TIER_BF16) does not read its failure count back to the
+// host: the kernels below are enqueued after screen_verify_kernel every time and return
+// at once when *n_fail == 0.  Otherwise the uncertified queries fail[0..nf) are gathered
+// into a compact block (fallback_gather_kernel) and ALL of them are re-run in one pass
+// over the slab on the exact-f32 MFMA tile (the direct scan's K9 body, fallback_search_
+// kernel): the query count is read on the device, so the tile shape and the grid are
+// picked in-kernel from nf - the narrow 32-query tile for nf <= 64 and the wide 128-query
+// tile above, exactly as plan_search would for a batch of nf - over a grid launched for
+// the worst case, whose surplus workgroups return at once (one of the two shapes always
+// returns whole).  fallback_merge_kernel then merges each failed query's lists (K10) and
+// writes its row in place into the caller's outputs.  Cost: one direct exact scan of nf
+// queries (r3's VALU fallback made one full slab pass per 4 failed queries).
+constexpr int kFbNarrowMax = 64;  // nf <= this: narrow tile (plan_search's `wide = nq > 64`)
 
-__device__ __forceinline__ void fb_insert(float& ls, int& li, int& cnt, float& ws, int& wi, float s,
-                                          int id, int k, int lane) {
-  if (cnt == k && !better(s, id, ws, wi)) return;  // wave-uniform
-  const int p = __popcll(__ballot(lane < cnt && better(ls, li, s, id)));
-  const float us = __shfl_up(ls, 1);
-  const int ui = __shfl_up(li, 1);
-  if (lane == p) {
-    ls = s;
-    li = id;
-  } else if (lane > p && lane < k) {
-    ls = us;
-    li = ui;
-  }
-  cnt = min(cnt + 1, k);
-  ws = __shfl(ls, k - 1);
-  wi = __shfl(li, k - 1);
+__global__ __launch_bounds__(256) void fallback_gather_kernel(const float* __restrict__ Q,
+                                                              const int* __restrict__ n_fail,
+                                                              const int64_t* __restrict__ fail,
+                                                              int dim, float* __restrict__ dst) {
+  const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nf) return;
+  const floatx4* s = reinterpret_cast<const floatx4*>(Q + fail[r] * dim);
+  floatx4* d = reinterpret_cast<floatx4*>(dst + r * dim);
+  for (int i = lane; i < (dim >> 2); i += 64) d[i] = s[i];
 }
 
-__global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ Q,
-                                                            const float* __restrict__ rows, int dim,
-                                                            int64_t n, const int* __restrict__ n_fail,
-                                                            const int64_t* __restrict__ fail, int k,
-                                                            int64_t nq_cap, float* __restrict__ cs,
-                                                            int64_t* __restrict__ ci) {
+template <class T, int KC>
+__global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void fallback_search_kernel(
+    const float* __restrict__ Qc, const int* __restrict__ n_fail, const float* __restrict__ C,
+    int64_t n_rows, int dim, int num_cus, int kl, float* __restrict__ cand_s,
+    int* __restrict__ cand_i) {
   const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
-  if (nf == 0) return;
-  __shared__ float ws_l[4 * MQ_MAX_K];
-  __shared__ int wi_l[4 * MQ_MAX_K];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t G = gridDim.x;
-  const int r0 = (int)(n * blockIdx.x / G), r1 = (int)(n * (blockIdx.x + 1) / G);
-  const int d4 = dim / 4;
-  for (int j0 = 0; j0 < nf; j0 += kFbQ) {
-    const floatx4* q4[kFbQ];
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u)
-      q4[u] = reinterpret_cast<const floatx4*>(Q + fail[min(j0 + u, nf - 1)] * (int64_t)dim);
-    float ls[kFbQ], wsc[kFbQ];
-    int li[kFbQ], cnt[kFbQ], wid[kFbQ];
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u) {
-      ls[u] = -INFINITY;
-      li[u] = -1;
-      cnt[u] = 0;
-      wsc[u] = -INFINITY;
-      wid[u] = -1;
-    }
-    for (int r = r0 + wave; r < r1; r += 4) {
-      const floatx4* c4 = reinterpret_cast<const floatx4*>(rows + (int64_t)r * dim);
-      float acc[kFbQ];
-#pragma unroll
-      for (int u = 0; u < kFbQ; ++u) acc[u] = 0.f;
-      for (int i = lane; i < d4; i += 64) {
-        const floatx4 b = c4[i];
-#pragma unroll
-        for (int u = 0; u < kFbQ; ++u) {
-          const floatx4 a = q4[u][i];
-          acc[u] = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc[u]))));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kFbQ; ++u) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
-        fb_insert(ls[u], li[u], cnt[u], wsc[u], wid[u], acc[u], r, k, lane);
-      }
-    }
-    // rank the 4 wave lists of each query into the workgroup's sorted list (padding
-    // (-inf, -1) entries tie: the LDS position breaks the tie so every slot is written)
-#pragma unroll
-    for (int u = 0; u < kFbQ; ++u) {
-      if (j0 + u >= nf) break;  // block-uniform
-      if (lane < k) {
-        ws_l[wave * k + lane] = ls[u];
-        wi_l[wave * k + lane] = li[u];
-      }
-      __syncthreads();
-      if (tid < 4 * k) {
-        const float x = ws_l[tid];
-        const int xi = wi_l[tid];
-        int rank = 0;
-        for (int v = 0; v < 4 * k; ++v)
-          rank += (better(ws_l[v], wi_l[v], x, xi) || (ws_l[v] == x && wi_l[v] == xi && v < tid)) ? 1 : 0;
-        if (rank < k) {
-          const int64_t o = ((int64_t)blockIdx.x * nq_cap + j0 + u) * k + rank;
-          cs[o] = x;
-          ci[o] = xi;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  if (nf == 0 || (nf > kFbNarrowMax) != (T::BM > 32)) return;
+  const ScanGeom g = scan_geom(nf, T::BM, T::BN, KC <= 16 ? 2 : 1, num_cus, n_rows);
+  if ((int)blockIdx.x >= g.G * g.nqt) return;  // workgroup-uniform
+  flat_search_block<T, KC>(Qc, nf, C, n_rows, dim, g.G, g.nqt, kl, cand_s, cand_i, blockIdx.x);
 }
 
 // One block per possible failure slot j (grid = the batch size): blocks j >= *n_fail
-// return; block j merges the G workgroup lists of fail[j] into the outputs' row fail[j].
-// Block 0 adds the count to the index's cumulative fallback counter.
-template <int KC>
+// return; block j merges the lists of compact query j (= fail[j]) into the outputs' row
+// fail[j].  Block 0 adds the count to the index's cumulative fallback counter.
+template <int KC, int SCAN_KC>
 __global__ __launch_bounds__(256) void fallback_merge_kernel(const float* __restrict__ cs,
-                                                             const int64_t* __restrict__ ci, int G,
-                                                             int64_t nq_cap, int k,
+                                                             const int* __restrict__ ci, int num_cus,
+                                                             int64_t n_rows, int k, int kl,
                                                              const int* __restrict__ n_fail,
                                                              const int64_t* __restrict__ fail,
                                                              float* __restrict__ os,
@@ -1073,8 +1032,17 @@ __global__ __launch_bounds__(256) void fallback_merge_kernel(const float* __rest
   const int64_t j = blockIdx.x;
   if (j == 0 && threadIdx.x == 0 && nf > 0) atomicAdd(total, (unsigned long long)nf);
   if (j >= nf) return;
+  constexpr int per_cu = SCAN_KC <= 16 ? 2 : 1;
+  int n_lists;
+  if (nf > kFbNarrowMax) {
+    const ScanGeom g = scan_geom(nf, SearchWide::BM, SearchWide::BN, per_cu, num_cus, n_rows);
+    n_lists = g.G * SearchWide::WAVES_N * SearchSmem<SearchWide>::LPQ;
+  } else {
+    const ScanGeom g = scan_geom(nf, SearchNarrow::BM, SearchNarrow::BN, per_cu, num_cus, n_rows);
+    n_lists = g.G * SearchNarrow::WAVES_N * SearchSmem<SearchNarrow>::LPQ;
+  }
   const int64_t shift = (fail[j] - j) * k;  // the block writes row j of (os + shift) = row fail[j]
-  merge_select_block<KC, int64_t>(cs, ci, G, nq_cap, k, k, os + shift, oi + shift, k, nullptr, j);
+  merge_select_block<KC, int>(cs, ci, n_lists, nf, kl, k, os + shift, oi + shift, kl, nullptr, j);
 }
 
 }  // namespace mq
@@ -1147,16 +1115,23 @@ struct mq_index {
   bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
   double i8_fail_avg = 0.0;      // running share of single queries the int8 screen failed to certify
   int i8_skip = 0;               // searches left that bypass the int8 tier after a bad run
+  int64_t i8_skips = 0;          // single-query searches that sat the int8 tier out
   // asynchronous batched screen (TIER_BF16): the uncertified queries are re-run on the
   // device (fallback_scan / fallback_merge) instead of behind a host read of the failure
   // count; after a batch is seen to have failed, the next kAsyncCooldown batched screens
   // run the synchronous tiered path (split-f32 tier first, cheaper for many failures)
   bool async_screen = true;
   int sync_left = 0;
-  DevBuf afb_cs, afb_ci, afb_total;  // fallback lists [G][nq][k]; cumulative count (u64)
+  DevBuf afb_q, afb_cs, afb_ci, afb_total;  // compact failed queries, their scan lists, cumulative count (u64)
   unsigned long long* afb_host = nullptr;  // pinned copy of the cumulative count
   hipEvent_t afb_event = nullptr;          // recorded after that copy
   unsigned long long afb_seen = 0;         // count already folded into screen_fallbacks
+  // bf16 tier self-disable: running share of batched queries the bf16 certificate failed
+  // (measured on the synchronous path); above kBfSkipShare the batched screen goes
+  // straight to the split-f32 tier for bf_skip searches
+  double bf_fail_avg = 0.0;
+  int bf_skip = 0;
+  int64_t bf_skips = 0;  // searches that bypassed the bf16 tier that way
   Timeline tl;  // stages: 0 = K9 score + top-k, 1 = K10 merge
   int precision = MQ_DTYPE_F32;
   std::mutex mu;
@@ -1208,19 +1183,16 @@ struct SearchPlan {
 
 SearchPlan plan_search(const mq_index* ix, int64_t nq, int kc) {
   SearchPlan p;
-  p.wide = nq > 64;
+  p.wide = nq > kFbNarrowMax;
   const int BM = p.wide ? SearchWide::BM : SearchNarrow::BM;
   const int BN = p.wide ? SearchWide::BN : SearchNarrow::BN;
   const int wn = p.wide ? SearchWide::WAVES_N : SearchNarrow::WAVES_N;
   const int lpq = p.wide ? SearchSmem<SearchWide>::LPQ : SearchSmem<SearchNarrow>::LPQ;
-  p.nqt = (int)((nq + BM - 1) / BM);
-  const int64_t ntiles = (ix->n + BN - 1) / BN;
   // resident 256-thread blocks per CU: 2 with an 8/16-entry register top list, 1 with
   // 64 (VGPR budget); G row groups per query tile, a multiple of 8 (XCD mapping)
-  const int per_cu = kc <= 16 ? 2 : 1;
-  int64_t G = std::max<int64_t>(1, per_cu * ix->num_cus / p.nqt);
-  G = std::min<int64_t>(G, ntiles);
-  p.G = (int)((G + 7) / 8 * 8);
+  const ScanGeom g = scan_geom(nq, BM, BN, kc <= 16 ? 2 : 1, ix->num_cus, ix->n);
+  p.nqt = g.nqt;
+  p.G = g.G;
   p.n_lists = (int64_t)p.G * wn * lpq;
   return p;
 }
@@ -1461,6 +1433,7 @@ bool i8_ok(mq_index* ix, int64_t nq) {
     return false;
   if (ix->i8_skip > 0) {
     --ix->i8_skip;
+    ++ix->i8_skips;
     return false;
   }
   return true;
@@ -1590,6 +1563,26 @@ bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
   return nq > 64 && k + 8 <= MQ_MAX_K && ix->dim <= 1024;
 }
 
+// The approximate tiers (int8, bf16) keep 64 candidates (16-48 on the bf16 stream) against
+// bounds of ~2e-3 .. 1.4e-2 on unit vectors, so the k-th best must clear the kc-th by
+// twice that.  Over 1M isotropic 768-d rows the k-th and 64-th best scores are ~0.58 /
+// 0.33 / 0.16 sigma (sigma = 0.036) apart at k = 5 / 16 / 32, and ~0.03 sigma at k = 50:
+// past k = 16 most certificates would fail and every batch would pay the screen AND the
+// re-run, so larger k goes straight to the split-f32 tier (bound 8e-5, kc = k + 8) or the
+// direct exact scan.
+constexpr int kScreenMaxK = 16;
+constexpr double kBfSkipShare = 0.2;  // bf16 certificate failure share that disables the tier
+constexpr int kBfSkipSearches = 64;
+
+int batch_tier(mq_index* ix, int64_t nq, int k) {
+  if (k <= kScreenMaxK) {
+    if (ix->bf_skip == 0) return TIER_BF16;
+    --ix->bf_skip;
+    ++ix->bf_skips;
+  }
+  return x6_tier_ok(ix, nq, k) ? TIER_X6 : -1;
+}
+
 constexpr int kAsyncCooldown = 16;
 
 // Fold a completed pinned copy of the device fallback count into screen_fallbacks (no
@@ -1604,13 +1597,57 @@ void poll_async_fallbacks(mq_index* ix) {
   }
 }
 
+// Worst case over every failure count nf = 1..nq of one tile shape's fallback scan:
+// workgroups to launch and candidate entries (lists x nf x kl).
+template <class T>
+void fallback_extent(const mq_index* ix, int64_t nf_lo, int64_t nf_hi, int per_cu, int kl,
+                     int64_t* grid, int64_t* cand) {
+  for (int64_t nqt = (nf_lo + T::BM - 1) / T::BM; nqt * T::BM < nf_hi + T::BM; ++nqt) {
+    const int64_t nf = std::min(nf_hi, nqt * T::BM);  // the most queries with this nqt
+    const ScanGeom g = scan_geom(nf, T::BM, T::BN, per_cu, ix->num_cus, ix->n);
+    *grid = std::max<int64_t>(*grid, (int64_t)g.G * g.nqt);
+    *cand = std::max<int64_t>(*cand, (int64_t)g.G * T::WAVES_N * SearchSmem<T>::LPQ * nf * kl);
+  }
+}
+
+template <int KC>
+void launch_fallback_scans(mq_index* ix, int64_t nq, int k, const int* nf, const int64_t* fail,
+                           float* os, int64_t* oi, int64_t grid_n, int64_t grid_w, hipStream_t s) {
+  const float* qc = ix->afb_q.as<float>();
+  float* cs = ix->afb_cs.as<float>();
+  int* ci = ix->afb_ci.as<int>();
+  hipLaunchKernelGGL((fallback_search_kernel<SearchNarrow, KC>), dim3((unsigned)grid_n), dim3(256), 0, s, qc,
+                     nf, ix->rows, ix->n, ix->dim, ix->num_cus, k, cs, ci);
+  if (grid_w > 0)
+    hipLaunchKernelGGL((fallback_search_kernel<SearchWide, KC>), dim3((unsigned)grid_w), dim3(256), 0, s, qc,
+                       nf, ix->rows, ix->n, ix->dim, ix->num_cus, k, cs, ci);
+  auto* tot = ix->afb_total.as<unsigned long long>();
+  const dim3 grid((unsigned)nq);
+  if (k <= 8)
+    hipLaunchKernelGGL((fallback_merge_kernel<8, KC>), grid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k, k,
+                       nf, fail, os, oi, tot);
+  else
+    hipLaunchKernelGGL((fallback_merge_kernel<16, KC>), grid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k,
+                       k, nf, fail, os, oi, tot);
+}
+
 // Device-side exact re-run of the uncertified queries (count and list from
-// screen_verify_kernel), results written into os / oi; nothing is read back.
+// screen_verify_kernel; k <= 16), results written into os / oi; nothing is read back.
+// Returns MQ_EAGAIN (nothing enqueued) when the worst-case candidate lists would take
+// more than kFbMaxBytes: the caller stays synchronous.
+constexpr size_t kFbMaxBytes = 256ull << 20;
+constexpr int MQ_EAGAIN_FB = 1;  // internal (positive: never an MQ_E* status)
+
 int launch_async_fallback(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
                           const int64_t* fail, hipStream_t s) {
-  const int G = ix->num_cus;
-  int rc = ix->afb_cs.ensure((size_t)G * nq * k * sizeof(float));
-  if (!rc) rc = ix->afb_ci.ensure((size_t)G * nq * k * sizeof(int64_t));
+  const int per_cu = 2;  // 8- / 16-entry scan lists
+  int64_t grid_n = 0, grid_w = 0, cand = 0;
+  fallback_extent<SearchNarrow>(ix, 1, std::min<int64_t>(nq, kFbNarrowMax), per_cu, k, &grid_n, &cand);
+  if (nq > kFbNarrowMax) fallback_extent<SearchWide>(ix, kFbNarrowMax + 1, nq, per_cu, k, &grid_w, &cand);
+  if ((size_t)cand * (sizeof(float) + sizeof(int)) > kFbMaxBytes) return MQ_EAGAIN_FB;
+  int rc = ix->afb_q.ensure((size_t)nq * ix->dim * sizeof(float));
+  if (!rc) rc = ix->afb_cs.ensure((size_t)cand * sizeof(float));
+  if (!rc) rc = ix->afb_ci.ensure((size_t)cand * sizeof(int));
   if (!rc && !ix->afb_total.p) {
     rc = ix->afb_total.ensure(sizeof(unsigned long long));
     if (!rc) MQ_HIP(hipMemset(ix->afb_total.p, 0, sizeof(unsigned long long)));
@@ -1622,26 +1659,14 @@ int launch_async_fallback(mq_index* ix, const float* q, int64_t nq, int k, float
   }
   if (!ix->afb_event) MQ_HIP(hipEventCreateWithFlags(&ix->afb_event, hipEventDisableTiming));
   const int* nf = ix->flag.as<int>();
-  hipLaunchKernelGGL(fallback_scan_kernel, dim3(G), dim3(256), 0, s, q, ix->rows, ix->dim, ix->n, nf, fail, k,
-                     nq, ix->afb_cs.as<float>(), ix->afb_ci.as<int64_t>());
-  auto* tot = ix->afb_total.as<unsigned long long>();
-  const dim3 grid((unsigned)nq);
-  switch (kc_merge(k)) {
-    case 8:
-      hipLaunchKernelGGL(fallback_merge_kernel<8>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
-                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
-      break;
-    case 16:
-      hipLaunchKernelGGL(fallback_merge_kernel<16>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
-                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
-      break;
-    default:
-      hipLaunchKernelGGL(fallback_merge_kernel<64>, grid, dim3(256), 0, s, ix->afb_cs.as<float>(),
-                         ix->afb_ci.as<int64_t>(), G, nq, k, nf, fail, os, oi, tot);
-      break;
-  }
+  hipLaunchKernelGGL(fallback_gather_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q, nf, fail,
+                     ix->dim, ix->afb_q.as<float>());
+  if (k <= 8)
+    launch_fallback_scans<8>(ix, nq, k, nf, fail, os, oi, grid_n, grid_w, s);
+  else
+    launch_fallback_scans<16>(ix, nq, k, nf, fail, os, oi, grid_n, grid_w, s);
   MQ_HIP(hipGetLastError());
-  MQ_HIP(hipMemcpyAsync(ix->afb_host, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(ix->afb_host, ix->afb_total.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipEventRecord(ix->afb_event, s));
   return MQ_OK;
 }
@@ -1698,11 +1723,10 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     MQ_HIP(hipGetLastError());
     if (tier == TIER_BF16) {
       poll_async_fallbacks(ix);
-      // (the fallback's per-workgroup lists take G nq k entries: very large batches stay
-      // on the synchronous path rather than reserve more than 256 MB for a rare event)
-      const bool fits = (size_t)ix->num_cus * nq * k * (sizeof(float) + sizeof(int64_t)) <= (256ull << 20);
-      if (ix->async_screen && ix->sync_left == 0 && fits)
-        return launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
+      if (ix->async_screen && ix->sync_left == 0 && k <= 16) {
+        rc = launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
+        if (rc != MQ_EAGAIN_FB) return rc;  // (very large batches stay synchronous)
+      }
       if (ix->sync_left > 0) --ix->sync_left;
     }
   }
@@ -1716,6 +1740,14 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     if (ix->i8_fail_avg > 0.3) {
       ix->i8_skip = 256;
       ix->i8_fail_avg = 0.0;
+    }
+  } else if (tier == TIER_BF16) {
+    // the same for batches: a crowded corpus (near-duplicates, clusters denser than the
+    // bf16 bound) sends the batched screen straight to the split-f32 tier for a while
+    ix->bf_fail_avg = 0.75 * ix->bf_fail_avg + 0.25 * (double)n_fail / (double)nq;
+    if (ix->bf_fail_avg > kBfSkipShare) {
+      ix->bf_skip = kBfSkipSearches;
+      ix->bf_fail_avg = 0.0;
     }
   }
   if (n_fail == 0) return MQ_OK;
@@ -1755,14 +1787,18 @@ int search_device(mq_index* ix, const float* q, int64_t nq, int k, float* os, in
   if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
   const bool screen = ix->precision == MQ_DTYPE_F32_SCREEN;
   if (nq <= ix->stream_max_q && stream_ok(ix)) {  // few queries: streaming scans
-    if (screen && i8_ok(ix, nq)) return search_screened(ix, TIER_I8, q, nq, k, os, oi, s);
-    if (screen && ix->dim % 128 == 0) return search_screened(ix, TIER_BF16_STREAM, q, nq, k, os, oi, s);
+    const bool approx = screen && k <= kScreenMaxK;
+    if (approx && i8_ok(ix, nq)) return search_screened(ix, TIER_I8, q, nq, k, os, oi, s);
+    if (approx && ix->dim % 128 == 0) return search_screened(ix, TIER_BF16_STREAM, q, nq, k, os, oi, s);
     return scan_topk(ix, SCAN_STREAM, q, nq, k, os, oi, s);
   }
   if (ix->precision == MQ_DTYPE_BF16 && ix->dim % 64 == 0)
     return search_bf16_rerank(ix, q, nq, k, os, oi, s);
-  if (screen && ix->dim % 64 == 0 && ix->dim <= 1024)
-    return search_screened(ix, TIER_BF16, q, nq, k, os, oi, s);
+  if (screen && ix->dim % 64 == 0 && ix->dim <= 1024) {
+    const int tier = batch_tier(ix, nq, k);
+    if (tier >= 0) return search_screened(ix, tier, q, nq, k, os, oi, s);
+    return search_direct(ix, q, nq, k, os, oi, s);
+  }
   return scan_topk(ix, ix->precision == MQ_DTYPE_F32X6 ? SCAN_X6 : SCAN_F32, q, nq, k, os, oi, s);
 }
 
@@ -1846,6 +1882,7 @@ int mq_index_destroy(mq_index* ix) {
     for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->rows8,
                       &ix->scale8, &ix->stats8})
       b->release();
+    ix->afb_q.release();
     ix->afb_cs.release();
     ix->afb_ci.release();
     ix->afb_total.release();
@@ -2079,19 +2116,28 @@ int mq_index_set_int8_screen(mq_index* ix, int enabled) {
   return MQ_OK;
 }
 
-int mq_index_screen_fallbacks(const mq_index* ix, int64_t* to_direct, int64_t* to_split) {
+// Blocks until the count copy of the last asynchronous screened search has landed (that
+// search's stream only - not a device-wide sync), then folds it in.
+int mq_index_screen_fallbacks(const mq_index* cix, int64_t* to_direct, int64_t* to_split) {
+  clear_error();
+  MQ_CHECK_ARG(cix, "NULL argument");
+  mq_index* ix = const_cast<mq_index*>(cix);  // the counters are folded in under the lock
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (ix->afb_event) {
+    DeviceGuard dg(ix->device);
+    MQ_HIP(hipEventSynchronize(ix->afb_event));
+    poll_async_fallbacks(ix);
+  }
+  if (to_direct) *to_direct = ix->screen_fallbacks;
+  if (to_split) *to_split = ix->screen_passdowns;
+  return MQ_OK;
+}
+
+int mq_index_screen_skips(const mq_index* ix, int64_t* bf16_skips, int64_t* int8_skips) {
   clear_error();
   MQ_CHECK_ARG(ix, "NULL argument");
-  int64_t pending = 0;  // asynchronous re-runs not yet folded in: read the device count
-  if (ix->afb_total.p) {
-    DeviceGuard dg(ix->device);
-    MQ_HIP(hipDeviceSynchronize());
-    unsigned long long tot = 0;
-    MQ_HIP(hipMemcpy(&tot, ix->afb_total.p, sizeof(tot), hipMemcpyDeviceToHost));
-    pending = (int64_t)(tot - ix->afb_seen);
-  }
-  if (to_direct) *to_direct = ix->screen_fallbacks + pending;
-  if (to_split) *to_split = ix->screen_passdowns;
+  if (bf16_skips) *bf16_skips = ix->bf_skips;
+  if (int8_skips) *int8_skips = ix->i8_skips;
   return MQ_OK;
 }
 
@@ -2101,6 +2147,8 @@ int mq_index_set_async_screen(mq_index* ix, int enabled) {
   std::lock_guard<std::mutex> lk(ix->mu);
   ix->async_screen = enabled != 0;
   ix->sync_left = 0;
+  ix->bf_skip = 0;
+  ix->bf_fail_avg = 0.0;
   return MQ_OK;
 }
 

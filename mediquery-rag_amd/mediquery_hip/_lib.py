@@ -73,6 +73,7 @@ SIGNATURES = {
     "mq_index_set_async_screen": (_I, [_P, _I]),
     "mq_index_rescans": (_I, [_P, _P, _P]),
     "mq_index_screen_fallbacks": (_I, [_P, _P, _P]),
+    "mq_index_screen_skips": (_I, [_P, _P, _P]),
     "mq_index_set_timing": (_I, [_P, _I]),
     "mq_index_read_timing": (_I, [_P, _P, _I]),
     "mq_index_save": (_I, [_P, ctypes.c_char_p]),

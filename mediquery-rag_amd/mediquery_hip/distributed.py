@@ -68,10 +68,12 @@ class LocalShards:
         if len(self):
             raise ValueError("LocalShards holds rows already: partition once")
         n = int(rows.shape[0])
+        self._cand = None  # its cached id offsets belong to the old (empty) partition
         for s in range(self.n_shards):
             off, cnt = shard_bounds(n, self.n_shards, s)
             self.offsets[s] = off
             if cnt:  # sized to the shard up front: no re-allocation while adding
+                self.shards[s].close()
                 self.shards[s] = FlatIndex(dim=self.dim, capacity=cnt, device=self.device)
                 self.shards[s].add_device(rows[off:off + cnt].contiguous())
 

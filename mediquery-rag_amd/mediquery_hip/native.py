@@ -135,6 +135,20 @@ class FlatIndex:
         _lib.call("mq_index_screen_fallbacks", self._h, None, ctypes.byref(n))
         return n.value
 
+    @property
+    def screen_skips(self):
+        """Batched screened searches that bypassed the bf16 tier (failure share > 0.2)."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_screen_skips", self._h, ctypes.byref(n), None)
+        return n.value
+
+    @property
+    def int8_skips(self):
+        """Single screened queries that sat the int8 tier out (failure share > 0.3)."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_screen_skips", self._h, None, ctypes.byref(n))
+        return n.value
+
     def set_timing(self, enabled=True):
         _lib.call("mq_index_set_timing", self._h, int(bool(enabled)))
 

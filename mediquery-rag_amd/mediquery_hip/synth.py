@@ -62,6 +62,32 @@ def corpus_device(n, dim, device, seed=CORPUS_SEED):
     return torch.randn((n, dim), generator=g, device=device, dtype=torch.float32)
 
 
+# exact duplicate rows of the reference corpus: data/medical_data.txt parses to 154 docs
+# whose page_content repeats at rows (72, 74), (104, 105), (110, 111), (120, 121) (SURVEY.md
+# §8c); the clustered device corpus repeats that pattern in every block of 154 rows
+REF_DUPLICATE_PAIRS = ((72, 74), (104, 105), (110, 111), (120, 121))
+
+
+def clustered_corpus_device(n, dim, device, seed=CORPUS_SEED, n_centroids=4096, sigma=0.35,
+                            duplicates=True):
+    """SURVEY.md §8d's clustered variant generated in HBM: rows = one of `n_centroids`
+    standard-normal centroids + sigma noise (cluster-mates at cosine ~0.89), plus the
+    reference corpus's exact-duplicate pattern.  -> (rows [n, dim], centroid id per row)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    cents = torch.randn((n_centroids, dim), generator=g, device=device)
+    assign = torch.randint(0, n_centroids, (n,), generator=g, device=device)
+    rows = torch.randn((n, dim), generator=g, device=device)
+    rows.mul_(sigma).add_(cents[assign])
+    if duplicates and n >= 154:
+        base = torch.arange(0, n - 153, 154, device=device)
+        for a, b in REF_DUPLICATE_PAIRS:
+            rows[base + b] = rows[base + a]
+            assign[base + b] = assign[base + a]
+    return rows, assign
+
+
 def corpus_shard_device(rows_per_shard, shard, dim, device, seed=CORPUS_SEED):
     """Shard `shard` of a corpus made of equal seeded blocks (BASELINE config 4: 10M rows
     as 8 x 1.25M): every rank regenerates only the blocks it owns, and the global corpus

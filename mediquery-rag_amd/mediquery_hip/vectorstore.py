@@ -27,6 +27,7 @@ re-ingested with this store (`python src/ingest_medical.py` after the import swa
 import json
 import math
 import os
+import re
 import uuid
 
 import numpy as np
@@ -59,7 +60,11 @@ def _match(meta, where):
                           "$in": lambda: v in x, "$nin": lambda: v not in x}.get(op)
                     if ok is None:
                         raise ValueError("unsupported filter operator %r" % op)
-                    if not ok():
+                    try:
+                        hit = ok()
+                    except TypeError:  # incomparable types: no match (see _pred)
+                        hit = False
+                    if not hit:
                         return False
             elif v != cond:
                 return False
@@ -78,8 +83,11 @@ def _pred(op, v, x):
     if op in ("$gt", "$gte", "$lt", "$lte"):
         if v is None:
             return False
-        return {"$gt": lambda: v > x, "$gte": lambda: v >= x, "$lt": lambda: v < x,
-                "$lte": lambda: v <= x}[op]()
+        try:
+            return {"$gt": lambda: v > x, "$gte": lambda: v >= x, "$lt": lambda: v < x,
+                    "$lte": lambda: v <= x}[op]()
+        except TypeError:  # incomparable types (a str value vs a number): no match, as in
+            return False   # Chroma, whose typed SQL comparison never matches across types
     if op == "$in":
         return v in x
     if op == "$nin":
@@ -171,6 +179,8 @@ def _check_k(k, n_candidates):
 class HipChroma(VectorStoreBase):
     _FILES = ("mq_%s.flat", "mq_%s.json")
     FOREIGN_DB = "chroma.sqlite3"  # what langchain_chroma / chromadb persist
+    _GEN = re.compile(r"[0-9a-f]{12}\.flat")  # slab generation suffix (persist() writes it)
+    STALE_SLAB_S = 3600  # an uncommitted slab this old is a crashed writer's leftover
 
     def __init__(self, collection_name="langchain", embedding_function=None,
                  persist_directory=None, client_settings=None, collection_metadata=None,
@@ -193,6 +203,7 @@ class HipChroma(VectorStoreBase):
         self._index = None
         self._dim = dim
         self._slab_name = None
+        self._written = set()  # slabs this instance wrote that no commit of its own names now
         if persist_directory and os.path.exists(self._path(1)):
             self._load()
         elif (persist_directory and not _ingest
@@ -241,21 +252,39 @@ class HipChroma(VectorStoreBase):
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, side)  # the commit point
-        self._slab_name = slab
+        replaced, self._slab_name = self._slab_name, slab
+        if replaced:
+            self._written.add(replaced)
         self._remove_orphan_slabs()
 
-    def _remove_orphan_slabs(self):
-        """Delete slabs of this collection the committed sidecar does not name: the one a
-        previous persist replaced, and any a crash or a concurrent writer left behind
-        between its slab write and its commit (each is a full copy of the index)."""
-        d = self._persist_directory
+    def _own_slab(self, f):
+        """Is file name `f` a slab of THIS collection (not of 'name.x', whose slabs also
+        start with 'mq_name.')?  Its generated names and the legacy single-slab name."""
         prefix = "mq_%s." % self._collection_name
+        return f == self._FILES[0] % self._collection_name or (
+            f.startswith(prefix) and self._GEN.fullmatch(f[len(prefix):]) is not None)
+
+    def _remove_orphan_slabs(self):
+        """After a commit: delete the slabs this instance replaced (the one it loaded or
+        wrote before), and this collection's slabs older than the sidecar by more than
+        STALE_SLAB_S (a crashed writer's leftovers).  A younger uncommitted slab may be
+        another process's write in flight (ingest and app share the directory), so it is
+        left alone; nothing is deleted on load."""
+        d = self._persist_directory
+        try:
+            side_mtime = os.path.getmtime(self._path(1))
+        except OSError:
+            return
         for f in os.listdir(d):
-            if f.startswith(prefix) and f.endswith(".flat") and f != self._slab_name:
-                try:
-                    os.remove(os.path.join(d, f))
-                except OSError:
-                    pass
+            if f == self._slab_name or not self._own_slab(f):
+                continue
+            p = os.path.join(d, f)
+            try:
+                if f in self._written or os.path.getmtime(p) < side_mtime - self.STALE_SLAB_S:
+                    os.remove(p)
+            except OSError:
+                pass
+        self._written.clear()
 
     def _reindex_host(self):
         self._id_row = {i: r for r, i in enumerate(self._ids)}
@@ -268,6 +297,7 @@ class HipChroma(VectorStoreBase):
             side = json.load(f)
         self._ensure_index(side["dim"])
         self._slab_name = side.get("slab", self._FILES[0] % self._collection_name)
+        self._written.add(self._slab_name)  # replaced (so deleted) by this instance's first commit
         self._index.load(os.path.join(self._persist_directory, self._slab_name))
         self._ids, self._texts, self._metas = side["ids"], side["documents"], side["metadatas"]
         self._collection_metadata = side.get("collection_metadata", {})
@@ -275,8 +305,6 @@ class HipChroma(VectorStoreBase):
             raise RuntimeError("persisted index (%d rows) and sidecar (%d ids) disagree"
                                % (len(self._index), len(self._ids)))
         self._reindex_host()
-        if os.access(self._persist_directory, os.W_OK):
-            self._remove_orphan_slabs()
 
     def _embed_query(self, query):
         if self._embedding_function is None:

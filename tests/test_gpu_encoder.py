@@ -42,6 +42,26 @@ def test_golden(require_gpu, g, case, cfg, prec):
     _close(enc.embed(g[src + "_ids"], g[src + "_mask"]), g[case + "_emb"])
 
 
+@pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6])
+def test_headline_shape_vs_oracle(require_gpu, prec):
+    """The exact encoder shape bench.py times (BASELINE config 3; the query embedding of
+    src/medical_engine.py:43): 12-layer dmeta-base, B = 256, L = 32, the bench's token ids -
+    the batched tiled path (not the few-row one) at full depth, host and device entry
+    points, against the oracle."""
+    import torch
+    from mediquery_hip import synth
+    ids, mask = synth.token_batch(256, 32)
+    ref = OracleEncoder(DMETA_BASE, synthetic_state_dict(DMETA_BASE, 0)).embed(ids, mask)
+    enc = Encoder(DMETA_BASE)
+    enc.set_precision(prec)
+    _close(enc.embed(ids, mask), ref)
+    dev = torch.device("cuda", 0)
+    out = torch.empty((256, 768), dtype=torch.float32, device=dev)
+    enc.embed_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), out)
+    torch.cuda.synchronize()
+    _close(out.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("B,L,ragged", [(1, 1, False), (1, 2, False), (3, 31, True), (5, 33, True),
                                         (2, 64, False), (4, 65, True), (9, 130, True),
                                         (2, 300, True), (1, 512, False), (70, 32, False)])

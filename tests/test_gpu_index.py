@@ -362,10 +362,12 @@ def _dup_corpus(n_fail, n=6000, copies=70, seed=0):
 @pytest.mark.parametrize("n_fail,k", [(1, 5), (6, 5), (9, 50), (5, 16)])
 def test_async_screen_fallback_exact(require_gpu, n_fail, k):
     """The default batched screen never reads its certificate back: uncertified queries
-    are re-run on the device (fallback_scan / fallback_merge, several queries per row
-    pass, k up to 64) and written in place.  Results equal the oracle, the duplicates come
-    out in id order, the count reaches screen_fallbacks, and after a failure has been
-    observed the next batches take the synchronous tiered path (same results)."""
+    are gathered and re-run on the device in one exact MFMA pass (fallback_search /
+    fallback_merge, k <= 16) and written in place; k = 50 skips the bf16 tier and runs the
+    split-f32 screen, whose failures go to the direct scan.  Results equal the oracle, the
+    duplicates come out in id order, the count reaches screen_fallbacks, and after a
+    failure has been observed the next batches take the synchronous tiered path (same
+    results)."""
     c, q = _dup_corpus(n_fail)
     ref = exact_scores(q, c)
     ix = _index(c, _lib.MQ_DTYPE_F32_SCREEN)
@@ -385,9 +387,9 @@ def test_async_screen_fallback_exact(require_gpu, n_fail, k):
 
 def test_async_screen_fallback_many_failures_threshold_scan(require_gpu):
     """130 of 256 queries uncertified on the threshold-scan path (>= 65536 rows): the device
-    fallback walks them 4 per row pass and every result equals the oracle; the
-    synchronous cooldown path then passes them down to the split-f32 tier (> 64 failures)
-    with the same ids."""
+    fallback re-runs them in one pass on the wide MFMA tile and every result equals the
+    oracle; the synchronous cooldown path then passes them down to the split-f32 tier
+    (> 64 failures) with the same ids."""
     rng = np.random.default_rng(9)
     c = synth.corpus(70000, 768, seed=9, clustered=True)
     q, _ = synth.queries(256, c, seed=9)

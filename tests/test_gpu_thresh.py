@@ -151,3 +151,33 @@ def test_bf16_mode_survivor_overflow_reruns_on_tiled_scan(require_gpu):
     assert (i >= 0).all()
     s2, i2 = ix.search(q, 50)  # deterministic across calls
     np.testing.assert_array_equal(i, i2)
+
+
+def test_config5_full_size_recall(require_gpu):
+    """BASELINE config 5 at its size: 1M x 768 bf16 shadow, batch 256, k = 50 - bf16 MFMA
+    coarse top-64 + exact fp32 re-rank: recall@50 >= 0.98 against the direct exact fp32
+    scan, returned scores exact fp32 dots of the returned rows (within two dot orders)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rows = synth.corpus_device(1_000_000, 768, dev)
+    q, planted = synth.queries_device(256, rows)
+    ix = FlatIndex(dim=768, capacity=1_000_000)
+    ix.add_device(rows)
+    k = 50
+    s = torch.empty((256, k), dtype=torch.float32, device=dev)
+    i = torch.empty((256, k), dtype=torch.int64, device=dev)
+    s2, i2 = torch.empty_like(s), torch.empty_like(i)
+    ix.set_precision(_lib.MQ_DTYPE_F32)
+    ix.search_device(q, k, s2, i2)
+    ix.set_precision(_lib.MQ_DTYPE_BF16)
+    ix.search_device(q, k, s, i)
+    torch.cuda.synchronize()
+    pl = planted >= 0
+    assert bool((i[pl, 0] == planted[pl]).all())
+    got, exact = i.cpu().numpy(), i2.cpu().numpy()
+    assert (got >= 0).all()
+    hits = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(got, exact))
+    assert hits / (256 * k) >= 0.98, hits / (256 * k)
+    normed = torch.nn.functional.normalize(rows, dim=1)
+    dots = (normed[i] * q[:, None, :]).sum(-1)  # fp32 dots of the returned rows
+    assert float((dots - s).abs().max()) < 1e-5

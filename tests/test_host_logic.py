@@ -126,3 +126,49 @@ def test_metadata_columns_equal_row_filter():
     kept.append({"title": "new", "n": 5})
     for w in wheres + [{"title": "new"}]:
         np.testing.assert_array_equal(cols.mask(w), [_match(m, w) for m in kept], err_msg=str(w))
+
+
+def test_metadata_mixed_types_compare_as_no_match():
+    """A range operator on a key whose values mix strings and numbers matches only the
+    comparable values (Chroma's typed comparison), in both the row and column filters,
+    instead of raising TypeError."""
+    from mediquery_hip.vectorstore import _MetaColumns
+    metas = [{"n": 3}, {"n": "7"}, {"n": 9.5}, {}, {"n": None}]
+    cols = _MetaColumns()
+    cols.append(metas)
+    for w in ({"n": {"$gt": 4}}, {"n": {"$lte": 3}}, {"n": {"$gt": "5"}}):
+        want = [_match(m, w) for m in metas]
+        np.testing.assert_array_equal(cols.mask(w), want, err_msg=str(w))
+    assert [_match(m, {"n": {"$gt": 4}}) for m in metas] == [False, False, True, False, False]
+    assert [_match(m, {"n": {"$gt": "5"}}) for m in metas] == [False, True, False, False, False]
+
+
+def test_orphan_slab_sweep_spares_sibling_collections_and_writes_in_flight(tmp_path):
+    """persist()'s sweep deletes only THIS collection's slabs that this instance replaced
+    or that are stale crash leftovers: never a sibling collection's ('docs' vs 'docs.v2'),
+    never another writer's fresh uncommitted slab, and nothing at load time."""
+    import os
+    import time
+    from mediquery_hip.vectorstore import HipChroma
+    d = str(tmp_path)
+    store = HipChroma(collection_name="docs")  # no index yet: host-only object
+    store._persist_directory = d
+    names = {"own_old": "mq_docs.0123456789ab.flat", "own_cur": "mq_docs.aaaaaaaaaaaa.flat",
+             "legacy": "mq_docs.flat", "sibling": "mq_docs.v2.bbbbbbbbbbbb.flat",
+             "sibling_legacy": "mq_docs.v2.flat", "inflight": "mq_docs.cccccccccccc.flat",
+             "stale": "mq_docs.dddddddddddd.flat", "other": "notes.flat"}
+    for n in names.values():
+        open(os.path.join(d, n), "wb").close()
+    open(os.path.join(d, "mq_docs.json"), "w").close()
+    old = time.time() - 2 * HipChroma.STALE_SLAB_S
+    os.utime(os.path.join(d, names["stale"]), (old, old))
+    assert store._own_slab(names["own_old"]) and store._own_slab(names["legacy"])
+    assert not store._own_slab(names["sibling"]) and not store._own_slab(names["sibling_legacy"])
+    store._slab_name = names["own_cur"]
+    store._written = {names["own_old"], names["legacy"]}
+    store._remove_orphan_slabs()
+    left = set(os.listdir(d))
+    assert names["own_old"] not in left and names["legacy"] not in left
+    assert names["stale"] not in left
+    for keep in ("own_cur", "sibling", "sibling_legacy", "inflight", "other"):
+        assert names[keep] in left, keep
