@@ -68,3 +68,57 @@ def test_wordpiece_matches_published_bert_tokenizer(golden, case):
     for j in range(40):
         n = int(mask[j].sum())
         assert ids[j, :n].tolist() == c["ids"][j] and not ids[j, n:].any()
+
+
+def _random_texts(rng, n):
+    """Random strings over the code-point classes the normaliser branches on: ASCII,
+    Latin-1 accents, combining marks, CJK (BMP + extension B), Hangul, fullwidth forms,
+    controls / format characters, private use, emoji, whitespace."""
+    ranges = [(0x20, 0x7e), (0xc0, 0x17f), (0x300, 0x36f), (0x4e00, 0x9fff), (0x20000, 0x2a6df),
+              (0xac00, 0xd7a3), (0xff01, 0xff5e), (0x0, 0x1f), (0x200b, 0x200f), (0xe000, 0xf8ff),
+              (0x1f600, 0x1f64f), (0x3000, 0x303f)]
+    out = []
+    for _ in range(n):
+        cps = []
+        for _ in range(int(rng.integers(0, 1500))):
+            lo, hi = ranges[int(rng.integers(len(ranges)))]
+            cp = int(rng.integers(lo, hi + 1))
+            cps.append(cp if cp else 0x20)  # (no NUL: the C ABI takes NUL-terminated strings)
+        out.append("".join(map(chr, cps)))
+    return out
+
+
+def test_native_tokenizers_on_random_text_and_raw_bytes(golden):
+    """Host-code robustness (also run under ASan + UBSan by tools/sanitize_cpu_tests.sh):
+    random strings over every character class give the Python twins' ids; raw byte
+    strings that are not UTF-8 (stray continuation bytes, truncated sequences, overlong
+    forms, surrogates, > U+10FFFF) go through the C ABI without a fault, with ids inside
+    the vocabulary and a mask that is a prefix of ones."""
+    import ctypes
+    from mediquery_hip import _lib
+    rng = np.random.default_rng(123)
+    g = json.load(open(os.path.join(golden, "wordpiece_golden.json"), encoding="utf-8"))
+    vocab = os.path.join(golden, g["vocab"])
+    texts = _random_texts(rng, 60)
+    for nat, py in ((NativeTokenizer.char(21128, max_length=512), CharTokenizer(21128, max_length=512)),
+                    (NativeTokenizer.wordpiece(vocab, max_length=512), WordPieceTokenizer(vocab, max_length=512))):
+        bad = [j for j, t in enumerate(texts) if nat.encode(t) != py.encode(t)]
+        assert not bad, [texts[j][:20] for j in bad[:3]]
+    raw = [bytes(rng.integers(1, 256, int(rng.integers(0, 3000)), dtype=np.uint8)) for _ in range(40)]
+    raw += [b"\x80\x80\x80", b"\xe4\xb8", b"\xc0\xaf", b"\xed\xa0\x80x", b"\xf4\x90\x80\x80", b"\xff" * 600]
+    n_vocab = sum(1 for _ in open(vocab, encoding="utf-8"))
+    for nat, vsize in ((NativeTokenizer.char(21128, max_length=512), 21128),
+                       (NativeTokenizer.wordpiece(vocab, max_length=512), n_vocab)):
+        cap = 512
+        ids = np.zeros(len(raw) * cap, np.int32)
+        mask = np.zeros(len(raw) * cap, np.int32)
+        arr = (ctypes.c_char_p * len(raw))(*raw)
+        L = ctypes.c_int()
+        _lib.call("mq_tokenizer_encode_batch", nat._h, arr, len(raw), 0, _lib.ptr(ids), _lib.ptr(mask),
+                  ctypes.byref(L))
+        ids, mask = ids[:len(raw) * L.value].reshape(len(raw), -1), mask[:len(raw) * L.value].reshape(len(raw), -1)
+        assert ((ids >= 0) & (ids < vsize)).all()
+        n = mask.sum(1)
+        assert (n >= 2).all()  # [CLS] ... [SEP] at least
+        for j in range(len(raw)):
+            assert mask[j, :n[j]].all() and not mask[j, n[j]:].any()
