@@ -64,17 +64,31 @@ def search_fp32_torch(queries, corpus_normed, k, threads=None):
     return v.numpy(), i.numpy()
 
 
-def check_topk(got_ids, got_scores, full_ref_scores, k, tol=1e-5, score_tol=1e-4,
-               ref_top=None, ref_lookup=None, n_rows=None):
+def check_topk(got_ids, got_scores, full_ref_scores, k, tol=1e-6, score_tol=1e-4,
+               ref_top=None, ref_lookup=None, n_rows=None, err_factor=3.0, tol_cap=1e-5):
     """Tie-group-aware comparison of a device top-k against the float64 oracle.
 
     Returns a list of failure strings (empty == parity).  Rules:
       * returned ids are distinct and within range; count == min(k, N);
       * each returned score is within `score_tol` of the oracle's score for that id;
       * position i must carry exactly the oracle's id wherever the oracle ranking is
-        unambiguous there (neighbouring oracle scores differ by more than `tol`);
-        inside a tie group, the returned id's oracle score must be within `tol` of the
-        oracle's score at that position.
+        unambiguous there (neighbouring oracle scores differ by more than the query's
+        tie tolerance); inside a tie group, the returned id's oracle score must be
+        within that tolerance of the oracle's score at that position.
+    Tie tolerance of query b: max(tol, err_factor * e_b) with tol = 1e-6
+    and e_b = the largest |device score - float64 score| among b's returned ids.  Why
+    the floor alone is not always attainable: a device score is fp32 arithmetic on fp32
+    data - the row norm (a 768-term sum of squares: relative error <= 768 u worst case,
+    ~sqrt(768) u / 2 ~ 8e-7 typical, u = 2^-24), the normalisation, and the 768-term
+    dot (<= 384 u sum|q_i r_i| for the MFMA's 2-term steps, ~1e-7 typical at |score|
+    ~0.2).  For scores near 1 (planted queries, duplicates) the norm term alone is ~1e-6,
+    so two rows whose float64 scores differ by 1e-6 can legitimately swap in fp32.  Two
+    scores swap only when their gap is below the sum of their errors; e_b measures those
+    errors on the rows in question (the missed row's is of the same size), so 3 e_b
+    covers the pair while the check stays at 1e-6 wherever the arithmetic is that
+    accurate (measured e_b ~1e-7 .. 5e-7 at |score| ~0.2).  Capped at tol_cap = 1e-5 (the
+    fixed tolerance of rounds 1-3): where scores carry encoder error (~1e-5 .. 1e-4 when
+    the oracle embedded the texts itself) the groups are no wider than before.
     For full-size checks pass `ref_top=(scores[B, k+1], ids[B, k+1])` (sorted) and
     `ref_lookup(b, ids) -> oracle scores` instead of the dense [B, N] score matrix.
     """
@@ -105,12 +119,13 @@ def check_topk(got_ids, got_scores, full_ref_scores, k, tol=1e-5, score_tol=1e-4
         if np.any(err > score_tol):
             fails.append("q%d: score error %.3g" % (b, err.max()))
         rs = ref_s[b]
+        tb = min(max(tol, err_factor * float(err.max(initial=0.0))), tol_cap)
         for i in range(kk):
             prev_gap = np.inf if i == 0 else rs[i - 1] - rs[i]
             next_gap = np.inf if i + 1 >= len(rs) else rs[i] - rs[i + 1]
-            if prev_gap > tol and next_gap > tol:
+            if prev_gap > tb and next_gap > tb:
                 if gi[i] != ref_i[b, i]:
                     fails.append("q%d pos%d: id %d != oracle %d" % (b, i, gi[i], ref_i[b, i]))
-            elif abs(gref[i] - rs[i]) > tol:
+            elif abs(gref[i] - rs[i]) > tb:
                 fails.append("q%d pos%d: id %d outside tie group" % (b, i, gi[i]))
     return fails
