@@ -495,35 +495,21 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
   __syncthreads();
   const int kl = n_live;
-  // eight candidates per wave per round, their row loads in flight together (the
-  // gathered rows come from HBM: the round is latency-bound, so more in flight per lane)
+  // eight candidates per wave per round, all their row loads in flight together (the
+  // gathered rows come from HBM: the round is latency-bound)
   constexpr int U = 8;
+  const int slot = rerank_slot(lane);
   for (int c0 = wave * U; c0 < kl; c0 += 4 * U) {
     long long id[U];
-    float acc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      id[u] = c0 + u < kl ? cand[q * kc + c0 + u] : -1;
-      acc[u] = 0.f;
-    }
-    for (int i = lane; i < dim / 4; i += 64) {
-      const floatx4 a = q4[i];
-      floatx4 b[U];
+    for (int u = 0; u < U; ++u) id[u] = c0 + u < kl ? cand[q * kc + c0 + u] : -1;
+    const float dot = rerank_dots8(q4, rows, dim, id, lane);
+    long long my_id = id[0];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
-      if (lane == 0 && c0 + u < kl) {
-        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
-        sid[c0 + u] = id[u];
-      }
+    for (int u = 1; u < U; ++u) my_id = slot == u ? id[u] : my_id;
+    if ((lane & 7) == 0 && c0 + slot < kl) {
+      sc[c0 + slot] = my_id >= 0 ? dot : -INFINITY;
+      sid[c0 + slot] = my_id;
     }
   }
   __syncthreads();
@@ -589,6 +575,7 @@ __global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict_
     const float x = ls[i];
     const int xi = li[i];
     int rank = 0;
+#pragma unroll 8
     for (int j = 0; j < cnt; ++j) rank += better(ls[j], li[j], x, xi) ? 1 : 0;
     if (rank < kc) {
       cs[rank] = rank == kc - 1 && total > kTsCap ? INFINITY : x;
@@ -607,33 +594,19 @@ __global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict_
   __syncthreads();
   const int kl = live_sh;
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  constexpr int U = MQ_MAX_K / 4;  // every candidate's row load in flight in one round
+  constexpr int U = 8;  // eight candidates per wave per round (rerank_kernel's arithmetic)
+  const int slot = rerank_slot(lane);
   for (int c0 = wave * U; c0 < kl; c0 += 4 * U) {
     long long id[U];
-    float acc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      id[u] = c0 + u < kl ? ci[c0 + u] : -1;
-      acc[u] = 0.f;
-    }
-    for (int i = lane; i < dim / 4; i += 64) {
-      const floatx4 a = q4[i];
-      floatx4 b[U];
+    for (int u = 0; u < U; ++u) id[u] = c0 + u < kl ? ci[c0 + u] : -1;
+    const float dot = rerank_dots8(q4, rows, dim, id, lane);
+    long long my_id = id[0];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        b[u] = reinterpret_cast<const floatx4*>(rows + (id[u] >= 0 ? id[u] : 0) * dim)[i];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        acc[u] = fmaf(a.x, b[u].x, fmaf(a.y, b[u].y, fmaf(a.z, b[u].z, fmaf(a.w, b[u].w, acc[u]))));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off);
-      if (lane == 0 && c0 + u < kl) {
-        sc[c0 + u] = id[u] >= 0 ? acc[u] : -INFINITY;
-        sid[c0 + u] = id[u];
-      }
+    for (int u = 1; u < U; ++u) my_id = slot == u ? id[u] : my_id;
+    if ((lane & 7) == 0 && c0 + slot < kl) {
+      sc[c0 + slot] = my_id >= 0 ? dot : -INFINITY;
+      sid[c0 + slot] = my_id;
     }
   }
   __syncthreads();

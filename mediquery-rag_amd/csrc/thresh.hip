@@ -447,27 +447,6 @@ __device__ __forceinline__ int i8_row(int lane) {
   return r;
 }
 
-__device__ __forceinline__ float xor_move(float v, int m) {
-  const int b = __float_as_int(v);
-  switch (m) {
-    case 8: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x128, 0xf, 0xf, false));  // row_ror:8
-    case 4: return __int_as_float(__builtin_amdgcn_ds_swizzle(b, 0x101f));  // xor 4 (bit mode)
-    case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x4e, 0xf, 0xf, false));   // quad [2,3,0,1]
-    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
-    default: return __shfl_xor(v, m);
-  }
-}
-
-// max over the wave, every lane gets it: DPP / swizzle within 16 lanes, then the two swaps
-__device__ __forceinline__ unsigned wave_max_u32(unsigned m) {
-#pragma unroll
-  for (int off = 1; off <= 8; off <<= 1) m = max(m, (unsigned)__float_as_int(xor_move(__int_as_float((int)m), off)));
-  auto r = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-  m = max((unsigned)r[0], (unsigned)r[1]);
-  r = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-  return max((unsigned)r[0], (unsigned)r[1]);
-}
-
 template <int NQ>
 __device__ __forceinline__ void transpose_reduce(float (&v)[kI8Rows * NQ], int lane) {
 #pragma unroll

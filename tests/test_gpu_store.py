@@ -9,6 +9,7 @@ with HipBertEmbeddings / HipChroma swapped in.  Expected: the committed config-1
 (transformers encoder + float64 exact top-5) within tie groups."""
 import json
 import os
+import time
 
 import numpy as np
 import pytest
@@ -120,7 +121,9 @@ def test_upsert_by_existing_id_replaces_row_and_persists(embeddings, docs, tmp_p
     """Chroma upsert semantics (`add_texts` with an id that exists, reference ingest
     src/ingest_medical.py:106-110 runs through add_texts): the row is replaced - one row
     per id, searches return the new text and metadata, a persisted reload agrees, and
-    orphaned slabs (a crash between slab write and commit) are cleaned up on load."""
+    slabs left uncommitted are never touched at load (one may be another process's write
+    in flight: ingest and app share the directory) and are swept by a later commit once
+    stale, as is the slab that commit replaced; a sibling collection's slab survives."""
     db = str(tmp_path / "db")
     ids = ["doc%03d" % i for i in range(30)]
     store = HipChroma.from_documents(documents=docs[:30], embedding=embeddings, ids=ids,
@@ -141,14 +144,23 @@ def test_upsert_by_existing_id_replaces_row_and_persists(embeddings, docs, tmp_p
     assert [d.page_content for d in store.similarity_search(new_text, k=3, filter={"title": "updated"})] == [new_text]
     store.delete(["doc007"])
     assert store.similarity_search(new_text, k=3, filter={"title": "updated"}) == []
-    open(os.path.join(db, "mq_langchain.deadbeef0000.flat"), "wb").write(b"orphan")
+    young, stale = "mq_langchain.deadbeef0000.flat", "mq_langchain.0badc0ffee00.flat"
+    sibling = "mq_langchain.v2.0123456789ab.flat"  # collection "langchain.v2"
+    for f in (young, stale, sibling):
+        open(os.path.join(db, f), "wb").write(b"orphan")
+    t_old = time.time() - 2 * HipChroma.STALE_SLAB_S
+    os.utime(os.path.join(db, stale), (t_old, t_old))
+    committed = store._slab_name
     again = HipChroma(persist_directory=db, embedding_function=embeddings)
     assert len(again) == 31 and again.get(ids=["doc007"])["ids"] == []
     assert again.get(ids=["dupe"])["documents"] == ["乙"]
-    assert [f for f in os.listdir(db) if f.endswith(".flat")] == [again._slab_name]
+    assert sorted(f for f in os.listdir(db) if f.endswith(".flat")) == sorted([committed, young, stale, sibling])
     s1 = [d.page_content for d in store.similarity_search(docs[3].page_content, k=5)]
     s2 = [d.page_content for d in again.similarity_search(docs[3].page_content, k=5)]
     assert s1 == s2
+    again.add_texts(["新增"], ids=["doc200"])  # a commit: replaced + stale slabs go
+    assert sorted(f for f in os.listdir(db) if f.endswith(".flat")) == sorted([again._slab_name, young, sibling])
+    assert len(HipChroma(persist_directory=db, embedding_function=embeddings)) == 32
 
 
 def test_filtered_search_equals_oracle_on_allowed_rows(embeddings, docs):
