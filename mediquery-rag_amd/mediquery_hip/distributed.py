@@ -110,17 +110,18 @@ class ShardedSearcher:
         self.group = group
 
     def _all_gather(self, t):
+        """[...] per rank -> [world, ...]: ONE all_gather_into_tensor into a concatenated
+        [world * n, ...] buffer (the form both RCCL and gloo accept, so the CPU tests run
+        the very call the RCCL path makes), viewed rank-major."""
         world = dist.get_world_size(self.group)
         t = t.contiguous()
-        if dist.get_backend(self.group) == "nccl":  # RCCL: one collective into one buffer
-            out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-            dist.all_gather_into_tensor(out, t, group=self.group)
-            return out
-        # gloo (CPU tests, or several ranks sharing one GPU in a rehearsal): host bounce
-        src = t.cpu()
-        out = torch.empty((world,) + tuple(src.shape), dtype=src.dtype)
-        dist.all_gather(list(out.unbind(0)), src, group=self.group)
-        return out.to(t.device)
+        # RCCL gathers device tensors over xGMI; gloo (CPU tests, or several ranks sharing
+        # one GPU in a rehearsal) gathers host copies
+        src = t if dist.get_backend(self.group) == "nccl" else t.cpu()
+        flat = src.reshape((-1,) + tuple(src.shape[1:])) if src.dim() else src.reshape(1)
+        out = torch.empty((world * flat.shape[0],) + tuple(flat.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, flat, group=self.group)
+        return out.view((world,) + tuple(t.shape)).to(t.device)
 
     def gather_queries(self, q_local):
         """[B, dim] per rank -> [world*B, dim] on every rank (rank-major)."""
