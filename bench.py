@@ -224,8 +224,12 @@ def _timed_steps(fn, steps, warmup):
 
 
 def _counters(ix):
-    return {"batch_fallbacks": ix.screen_fallbacks, "passdowns": ix.screen_passdowns,
-            "bf16_tier_skips": ix.screen_skips, "int8_tier_skips": ix.int8_skips}
+    out = {"batch_fallbacks": ix.screen_fallbacks, "passdowns": ix.screen_passdowns}
+    try:
+        out.update(bf16_tier_skips=ix.screen_skips, int8_tier_skips=ix.int8_skips)
+    except AttributeError:  # an older library under A/B (MQ_LIB_ALLOW_MISSING=1)
+        out.update(bf16_tier_skips=0, int8_tier_skips=0)
+    return out
 
 
 def config2(args, enc, dev, ids, mask, q):

@@ -112,13 +112,12 @@ __host__ __device__ inline ScanGeom scan_geom(int64_t nq, int BM, int BN, int pe
 }
 
 template <class T, int KC>
-__device__ __forceinline__ void flat_search_block(const float* __restrict__ Q, int nq,
+__device__ __forceinline__ void flat_search_block(float* lds, const float* __restrict__ Q, int nq,
                                                   const float* __restrict__ C, int64_t n_rows,
                                                   int dim, int G, int nqt, int kl,
                                                   float* __restrict__ cand_s,
                                                   int* __restrict__ cand_i, int b) {
   using S = SearchSmem<T>;
-  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
@@ -189,7 +188,8 @@ template <class T, int KC>
 __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
     const float* __restrict__ Q, int nq, const float* __restrict__ C, int64_t n_rows, int dim,
     int G, int nqt, int kl, float* __restrict__ cand_s, int* __restrict__ cand_i) {
-  flat_search_block<T, KC>(Q, nq, C, n_rows, dim, G, nqt, kl, cand_s, cand_i, blockIdx.x);
+  __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
+  flat_search_block<T, KC>(lds, Q, nq, C, n_rows, dim, G, nqt, kl, cand_s, cand_i, blockIdx.x);
 }
 
 // ============================================ K9s: streaming scan, few queries ==
@@ -442,19 +442,32 @@ __device__ __forceinline__ float screen_bound(const float* __restrict__ Q, int d
   return (dq * cmax + bqn * dmax + g * bqn * (cmax + dmax) + g * qn * cmax) * 1.001f + 1e-7f;
 }
 
+// compact (optional, the asynchronous batch path): the failed query's vector is also
+// copied to row `slot` of compact, the block the device re-run scans.
 __global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restrict__ Q, int dim,
                                                             const float* __restrict__ cs, int kc,
                                                             const float* __restrict__ es, int k,
                                                             int64_t nq, int mode,
                                                             const unsigned* __restrict__ stats,
                                                             int* __restrict__ n_fail,
-                                                            int64_t* __restrict__ fail) {
+                                                            int64_t* __restrict__ fail,
+                                                            float* __restrict__ compact) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   const float E = screen_bound(Q, dim, q, mode, stats, lane);
-  if (lane != 0) return;
-  if (!(cs[q * kc + kc - 1] + E < es[q * k + k - 1])) fail[atomicAdd(n_fail, 1)] = q;
+  const bool failed = !(cs[q * kc + kc - 1] + E < es[q * k + k - 1]);  // wave-uniform
+  if (!failed) return;
+  int slot = 0;
+  if (lane == 0) {
+    slot = atomicAdd(n_fail, 1);
+    fail[slot] = q;
+  }
+  if (!compact) return;
+  slot = __shfl(slot, 0);
+  const floatx4* src = reinterpret_cast<const floatx4*>(Q + q * dim);
+  floatx4* dst = reinterpret_cast<floatx4*>(compact + (int64_t)slot * dim);
+  for (int i = lane; i < (dim >> 2); i += 64) dst[i] = src[i];
 }
 
 // Exact fp32 re-rank of the coarse candidates: one block per query, one wave per
@@ -951,42 +964,38 @@ __global__ __launch_bounds__(256) void merge_select_kernel(const float* __restri
 
 // ---------------------------------------------- asynchronous screen fallback ------
 // The batched certified screen (TIER_BF16) does not read its failure count back to the
-// host: the kernels below are enqueued after screen_verify_kernel every time and return
-// at once when *n_fail == 0.  Otherwise the uncertified queries fail[0..nf) are gathered
-// into a compact block (fallback_gather_kernel) and ALL of them are re-run in one pass
-// over the slab on the exact-f32 MFMA tile (the direct scan's K9 body, fallback_search_
-// kernel): the query count is read on the device, so the tile shape and the grid are
-// picked in-kernel from nf - the narrow 32-query tile for nf <= 64 and the wide 128-query
-// tile above, exactly as plan_search would for a batch of nf - over a grid launched for
-// the worst case, whose surplus workgroups return at once (one of the two shapes always
-// returns whole).  fallback_merge_kernel then merges each failed query's lists (K10) and
-// writes its row in place into the caller's outputs.  Cost: one direct exact scan of nf
-// queries (r3's VALU fallback made one full slab pass per 4 failed queries).
+// host.  screen_verify_kernel copies each uncertified query into a compact block as it
+// lists it, and two kernels are enqueued behind it every time, both returning at once
+// when *n_fail == 0: fallback_search_kernel re-runs ALL nf failed queries in one pass over
+// the slab on the exact-f32 MFMA tile (the direct scan's K9 body) - the query count is
+// read on the device, so the tile shape and the grid are picked in-kernel from nf (the
+// narrow 32-query tile for nf <= 64, the wide 128-query tile above, exactly as
+// plan_search would for a batch of nf) over a grid launched for the worst case, whose
+// surplus workgroups return at once - and fallback_merge_kernel merges each failed
+// query's lists (K10) and writes its row in place into the caller's outputs.  Cost: one
+// direct exact scan of nf queries (r3's VALU fallback made one slab pass per 4 queries).
 constexpr int kFbNarrowMax = 64;  // nf <= this: narrow tile (plan_search's `wide = nq > 64`)
 
-__global__ __launch_bounds__(256) void fallback_gather_kernel(const float* __restrict__ Q,
-                                                              const int* __restrict__ n_fail,
-                                                              const int64_t* __restrict__ fail,
-                                                              int dim, float* __restrict__ dst) {
-  const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= nf) return;
-  const floatx4* s = reinterpret_cast<const floatx4*>(Q + fail[r] * dim);
-  floatx4* d = reinterpret_cast<floatx4*>(dst + r * dim);
-  for (int i = lane; i < (dim >> 2); i += 64) d[i] = s[i];
-}
-
-template <class T, int KC>
+template <int KC>
 __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void fallback_search_kernel(
     const float* __restrict__ Qc, const int* __restrict__ n_fail, const float* __restrict__ C,
     int64_t n_rows, int dim, int num_cus, int kl, float* __restrict__ cand_s,
     int* __restrict__ cand_i) {
+  constexpr int kLds = 2 * (SearchWide::STAGE_FLOATS > SearchNarrow::STAGE_FLOATS ? SearchWide::STAGE_FLOATS
+                                                                                     : SearchNarrow::STAGE_FLOATS);
+  __shared__ __attribute__((aligned(16))) float lds[kLds];
   const int nf = __builtin_amdgcn_readfirstlane(*n_fail);
-  if (nf == 0 || (nf > kFbNarrowMax) != (T::BM > 32)) return;
-  const ScanGeom g = scan_geom(nf, T::BM, T::BN, KC <= 16 ? 2 : 1, num_cus, n_rows);
-  if ((int)blockIdx.x >= g.G * g.nqt) return;  // workgroup-uniform
-  flat_search_block<T, KC>(Qc, nf, C, n_rows, dim, g.G, g.nqt, kl, cand_s, cand_i, blockIdx.x);
+  if (nf == 0) return;
+  constexpr int per_cu = KC <= 16 ? 2 : 1;
+  if (nf > kFbNarrowMax) {
+    const ScanGeom g = scan_geom(nf, SearchWide::BM, SearchWide::BN, per_cu, num_cus, n_rows);
+    if ((int)blockIdx.x >= g.G * g.nqt) return;  // workgroup-uniform
+    flat_search_block<SearchWide, KC>(lds, Qc, nf, C, n_rows, dim, g.G, g.nqt, kl, cand_s, cand_i, blockIdx.x);
+  } else {
+    const ScanGeom g = scan_geom(nf, SearchNarrow::BM, SearchNarrow::BN, per_cu, num_cus, n_rows);
+    if ((int)blockIdx.x >= g.G * g.nqt) return;
+    flat_search_block<SearchNarrow, KC>(lds, Qc, nf, C, n_rows, dim, g.G, g.nqt, kl, cand_s, cand_i, blockIdx.x);
+  }
 }
 
 // One block per possible failure slot j (grid = the batch size): blocks j >= *n_fail
@@ -1585,39 +1594,42 @@ void fallback_extent(const mq_index* ix, int64_t nf_lo, int64_t nf_hi, int per_c
 
 template <int KC>
 void launch_fallback_scans(mq_index* ix, int64_t nq, int k, const int* nf, const int64_t* fail,
-                           float* os, int64_t* oi, int64_t grid_n, int64_t grid_w, hipStream_t s) {
+                           float* os, int64_t* oi, int64_t grid, hipStream_t s) {
   const float* qc = ix->afb_q.as<float>();
   float* cs = ix->afb_cs.as<float>();
   int* ci = ix->afb_ci.as<int>();
-  hipLaunchKernelGGL((fallback_search_kernel<SearchNarrow, KC>), dim3((unsigned)grid_n), dim3(256), 0, s, qc,
-                     nf, ix->rows, ix->n, ix->dim, ix->num_cus, k, cs, ci);
-  if (grid_w > 0)
-    hipLaunchKernelGGL((fallback_search_kernel<SearchWide, KC>), dim3((unsigned)grid_w), dim3(256), 0, s, qc,
-                       nf, ix->rows, ix->n, ix->dim, ix->num_cus, k, cs, ci);
+  hipLaunchKernelGGL((fallback_search_kernel<KC>), dim3((unsigned)grid), dim3(256), 0, s, qc, nf, ix->rows,
+                     ix->n, ix->dim, ix->num_cus, k, cs, ci);
   auto* tot = ix->afb_total.as<unsigned long long>();
-  const dim3 grid((unsigned)nq);
+  const dim3 mgrid((unsigned)nq);
   if (k <= 8)
-    hipLaunchKernelGGL((fallback_merge_kernel<8, KC>), grid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k, k,
+    hipLaunchKernelGGL((fallback_merge_kernel<8, KC>), mgrid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k, k,
                        nf, fail, os, oi, tot);
   else
-    hipLaunchKernelGGL((fallback_merge_kernel<16, KC>), grid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k,
+    hipLaunchKernelGGL((fallback_merge_kernel<16, KC>), mgrid, dim3(256), 0, s, cs, ci, ix->num_cus, ix->n, k,
                        k, nf, fail, os, oi, tot);
 }
 
-// Device-side exact re-run of the uncertified queries (count and list from
-// screen_verify_kernel; k <= 16), results written into os / oi; nothing is read back.
-// Returns MQ_EAGAIN (nothing enqueued) when the worst-case candidate lists would take
-// more than kFbMaxBytes: the caller stays synchronous.
+// Device-side exact re-run of the uncertified queries (count, list and compact query
+// block from screen_verify_kernel; k <= 16), results written into os / oi; nothing is
+// read back.  fallback_prepare sizes the workspace (before the verify launch, which
+// writes the compact block) and says whether the asynchronous path applies: not when the
+// worst-case candidate lists would take more than kFbMaxBytes (very large batches stay
+// synchronous).
 constexpr size_t kFbMaxBytes = 256ull << 20;
-constexpr int MQ_EAGAIN_FB = 1;  // internal (positive: never an MQ_E* status)
 
-int launch_async_fallback(mq_index* ix, const float* q, int64_t nq, int k, float* os, int64_t* oi,
-                          const int64_t* fail, hipStream_t s) {
+struct FallbackPlan {
+  bool ok = false;
+  int64_t grid = 0;
+};
+
+int fallback_prepare(mq_index* ix, int64_t nq, int k, FallbackPlan* fp) {
   const int per_cu = 2;  // 8- / 16-entry scan lists
   int64_t grid_n = 0, grid_w = 0, cand = 0;
   fallback_extent<SearchNarrow>(ix, 1, std::min<int64_t>(nq, kFbNarrowMax), per_cu, k, &grid_n, &cand);
   if (nq > kFbNarrowMax) fallback_extent<SearchWide>(ix, kFbNarrowMax + 1, nq, per_cu, k, &grid_w, &cand);
-  if ((size_t)cand * (sizeof(float) + sizeof(int)) > kFbMaxBytes) return MQ_EAGAIN_FB;
+  fp->ok = false;
+  if ((size_t)cand * (sizeof(float) + sizeof(int)) > kFbMaxBytes) return MQ_OK;
   int rc = ix->afb_q.ensure((size_t)nq * ix->dim * sizeof(float));
   if (!rc) rc = ix->afb_cs.ensure((size_t)cand * sizeof(float));
   if (!rc) rc = ix->afb_ci.ensure((size_t)cand * sizeof(int));
@@ -1631,13 +1643,18 @@ int launch_async_fallback(mq_index* ix, const float* q, int64_t nq, int k, float
     *ix->afb_host = 0;
   }
   if (!ix->afb_event) MQ_HIP(hipEventCreateWithFlags(&ix->afb_event, hipEventDisableTiming));
+  fp->ok = true;
+  fp->grid = std::max(grid_n, grid_w);
+  return MQ_OK;
+}
+
+int launch_async_fallback(mq_index* ix, const FallbackPlan& fp, int64_t nq, int k, float* os, int64_t* oi,
+                          const int64_t* fail, hipStream_t s) {
   const int* nf = ix->flag.as<int>();
-  hipLaunchKernelGGL(fallback_gather_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q, nf, fail,
-                     ix->dim, ix->afb_q.as<float>());
   if (k <= 8)
-    launch_fallback_scans<8>(ix, nq, k, nf, fail, os, oi, grid_n, grid_w, s);
+    launch_fallback_scans<8>(ix, nq, k, nf, fail, os, oi, fp.grid, s);
   else
-    launch_fallback_scans<16>(ix, nq, k, nf, fail, os, oi, grid_n, grid_w, s);
+    launch_fallback_scans<16>(ix, nq, k, nf, fail, os, oi, fp.grid, s);
   MQ_HIP(hipGetLastError());
   MQ_HIP(hipMemcpyAsync(ix->afb_host, ix->afb_total.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   MQ_HIP(hipEventRecord(ix->afb_event, s));
@@ -1689,19 +1706,21 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
                        ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), mode, stats);
     MQ_HIP(hipGetLastError());
     if (kc >= ix->n) return MQ_OK;  // every row was a candidate: the re-rank is the answer
-    MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
-    hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
-                       ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
-                       fail);
-    MQ_HIP(hipGetLastError());
+    FallbackPlan fp;
     if (tier == TIER_BF16) {
       poll_async_fallbacks(ix);
       if (ix->async_screen && ix->sync_left == 0 && k <= 16) {
-        rc = launch_async_fallback(ix, q, nq, k, os, oi, fail, s);
-        if (rc != MQ_EAGAIN_FB) return rc;  // (very large batches stay synchronous)
+        rc = fallback_prepare(ix, nq, k, &fp);
+        if (rc) return rc;
       }
-      if (ix->sync_left > 0) --ix->sync_left;
+      if (!fp.ok && ix->sync_left > 0) --ix->sync_left;
     }
+    MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q,
+                       ix->dim, ix->coarse_s.as<float>(), kc, os, k, nq, mode, stats, ix->flag.as<int>(),
+                       fail, fp.ok ? ix->afb_q.as<float>() : nullptr);
+    MQ_HIP(hipGetLastError());
+    if (fp.ok) return launch_async_fallback(ix, fp, nq, k, os, oi, fail, s);
   }
   int n_fail = 0;
   rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);

@@ -9,7 +9,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --single-iters 10 --secondary-seq-len 0 --config4-steps 0"
+BENCH="$ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --single-iters 10 --secondary-seq-len 0 --config4-steps 0 --no-extras"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 echo "trace done"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch_bench.json" 2> "$OUT/fetch.err"
