@@ -65,6 +65,8 @@ def parse():
                    help="also time the headline step at this L (0 = skip)")
     p.add_argument("--config4-steps", type=int, default=10,
                    help="BASELINE config 4 line (10M x 768 as 8 row shards, batch 1024): timed steps (0 = skip)")
+    p.add_argument("--enc-opt", action="append", default=[],
+                   help="NAME=VALUE encoder option (Encoder.OPTIONS) for A/B runs; repeatable")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the config-2, clustered-corpus, long-query and k=50 extras")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -404,6 +406,9 @@ def main():
     index = FlatIndex(dim=768, capacity=cnt, device=local)
     index.add_device(full[off:off + cnt].contiguous())
     enc = Encoder(cfg, device=local)
+    for kv in args.enc_opt:
+        name, val = kv.split("=")
+        enc.set_option(name, int(val))
     ids_np, mask_np = synth.token_batch(B, L, seed=synth.TOKEN_SEED + rank)
     ids = torch.from_numpy(ids_np).to(dev)
     mask = torch.from_numpy(mask_np).to(dev)

@@ -225,6 +225,11 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *   MQ_ENC_OPT_SPLITK_TILES      tiled path, M <= 256 rows: a GEMM is split over K only when
  *                                its direct grid has at most this many 32 x 128 tiles
  *                                (0..4096, default 0 = one tile per CU)
+ *   MQ_ENC_OPT_LN_ON_LOAD        batched forward, exact f32, M > 256, hidden 768: the
+ *                                LayerNorms applied by the consuming GEMM while it stages its
+ *                                input, from per-row partials the residual GEMM leaves (1), or
+ *                                a LayerNorm launch each (0, default: the staging VALU cost the
+ *                                QKV / FFN-up GEMMs 16-18%, more than the 24 launches save)
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
@@ -233,6 +238,7 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 #define MQ_ENC_OPT_FUSE_ATTN_OPROJ 4
 #define MQ_ENC_OPT_FUSED_LN 5
 #define MQ_ENC_OPT_SPLITK_TILES 6
+#define MQ_ENC_OPT_LN_ON_LOAD 7
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);

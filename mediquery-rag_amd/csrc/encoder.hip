@@ -27,7 +27,31 @@
 
 namespace mq {
 
-enum Epi { EPI_BIAS = 0, EPI_GELU_ERF = 1, EPI_GELU_TANH = 2, EPI_RESID = 3 };
+// EPI_RESID_STATS: EPI_RESID that also leaves per-row LayerNorm partials of its output
+// (the LayerNorm is then applied by the consuming GEMM while it stages A: LnArgs below).
+enum Epi { EPI_BIAS = 0, EPI_GELU_ERF = 1, EPI_GELU_TANH = 2, EPI_RESID = 3, EPI_RESID_STATS = 4 };
+
+// LayerNorm deferred into the consumer (batched path, MQ_ENC_OPT_LN_ON_LOAD).  The
+// residual GEMM (out-proj / FFN-down, EPI_RESID_STATS) writes y = A W^T + b + resid and,
+// per row and per wave tile of kLnPartW columns, the partial (mean, M2) of y: stats[row][t].
+// The next GEMM (FFN-up / the next layer's QKV, LN_IN) merges a row's partials into (mean,
+// rstd) once per tile (Chan: M2 = sum M2_t + w sum (mean_t - mean)^2, equal counts w) and
+// normalises every A element between its global load and its LDS write, (y - mean) rstd
+// gamma + beta; the tiles of column 0 also store LN(y) to x, the residual input of the
+// following residual GEMM.  No LayerNorm launch and no y -> x round trip.  Two-pass-class
+// statistics in fp32; ln_kernel's summation order differs (results agree to rounding).
+constexpr int kLnPartW = 96;   // columns per partial: the producer's wave tile (F32Tile<4,1,1,3>)
+constexpr int kLnMaxParts = 8;  // partials per row: the path runs at H = 768 (BERT-base)
+struct LnArgs {
+  float* stats_out;       // producer: [M][nt] (mean, M2) pairs
+  const float* stats_in;  // consumer: the producer's pairs for A's rows
+  const float* g;         // consumer: LayerNorm gamma [K]
+  const float* b;         //           beta [K]
+  float* xout;            //           column-0 tiles store LN(A) rows here
+  int ldx;
+  int nt;                 // partials per row (K / kLnPartW)
+  float eps;
+};
 
 // GELU, branch-free (it runs 64 times per lane in every FFN-up tile epilogue; ocml's erff
 // is ~50 VALU + a divergent branch per element and measured as the FFN-up epilogue's cost).
@@ -74,14 +98,117 @@ __device__ __forceinline__ float wave_sum(float v) {
 // the last slice of the current one, so the epilogue overlaps the next tile's loads.
 // Within a round, the workgroups of one XCD (blockIdx % 8 equal) take consecutive
 // tiles, i.e. share A row panels in their L2.
-template <class T, int EPI>
+// LN_IN: the consumer side of LnArgs, as walk_tiles_hooked hooks.  Per tile, threads t <
+// BM load row m0 + t's partials with the tile's first slice (issue), merge them into
+// (mean, rstd) in LDS at that iteration's store phase (prepare; two slots by tile parity),
+// and every A slot is normalised on its registers before the LDS write (xform).  A slot's
+// row and 16-B chunk are fixed per thread (THREADS % F4_PER_ROW == 0), so gamma / beta are
+// one float4 each per slice, loaded with the slice.
+// MQ_LN_DIAG (measurement builds only): 1 = the hooks stage nothing (no partial / gamma /
+// beta loads, no normalisation: wrong results) - the hooked walker's own cost; 2 = loads
+// kept, normalisation skipped.
+#ifndef MQ_LN_DIAG
+#define MQ_LN_DIAG 0
+#endif
+#if MQ_LN_DIAG != 0 && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_LN_DIAG computes wrong results: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
+#endif
+
+template <class T, class Coords>
+struct LnInHooks {
+  static constexpr int A_LOADS = T::BM * T::F4_PER_ROW / T::THREADS;
+  static_assert(T::A_SLOTS && T::THREADS % T::F4_PER_ROW == 0, "A slots: fixed row chunk per thread");
+  const LnArgs& ln;
+  Coords& coords;
+  float2* st;  // LDS [2][BM] (mean, rstd)
+  int M, nk, S;
+  float inv_k;
+  FastDiv nkd;
+  float2 part[kLnMaxParts];
+  floatx4 gg[T::PF], bb[T::PF];
+  float2 mr[A_LOADS];  // (mean, rstd) of this thread's A rows for the slice being stored
+  template <class DC>
+  __device__ __forceinline__ void issue(int s, DC) {
+    if constexpr (MQ_LN_DIAG == 1) return;
+    constexpr int d = DC::value;
+    const int sc = s < S ? s : S - 1;
+    const int i = nkd.div(sc), kt = sc - i * nk;
+    const int k = kt * T::BK + (threadIdx.x % T::F4_PER_ROW) * 4;
+    gg[d] = *reinterpret_cast<const floatx4*>(ln.g + k);
+    bb[d] = *reinterpret_cast<const floatx4*>(ln.b + k);
+    // (coords outside any per-thread branch: a tile origin computed under divergent control
+    // flow turns the staging's buffer descriptors into VGPRs - waterfall loops per load)
+    int m0;
+    int64_t n0;
+    coords(i, m0, n0);
+    // the partials of the fetched slice's tile rows, loaded with EVERY slice (64 B per
+    // thread from L2; rows past BM repeat): loaded only at tile starts, the registers
+    // would merge two values at the join and the copy would wait for the loads right there
+    const float2* src = reinterpret_cast<const float2*>(ln.stats_in) +
+                        (int64_t)min(m0 + (int)threadIdx.x % T::BM, M - 1) * kLnMaxParts;
+#pragma unroll
+    for (int t = 0; t < kLnMaxParts; ++t) part[t] = src[t];
+  }
+  __device__ __forceinline__ void prepare(int s) {
+    if constexpr (MQ_LN_DIAG == 1) return;
+    if (s >= S || nkd.mod(s) != 0) return;  // workgroup-uniform
+    // the merge must stay here, after the slice's MFMAs: left alone the compiler folds it
+    // into issue()'s equal-condition block and waits there for the partials' loads
+#pragma unroll
+    for (int t = 0; t < kLnMaxParts; ++t) asm volatile("" : "+v"(part[t].x), "+v"(part[t].y));
+    float mean = 0.f;
+#pragma unroll
+    for (int t = 0; t < kLnMaxParts; ++t) mean += part[t].x;
+    mean *= 1.0f / (float)kLnMaxParts;
+    float m2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < kLnMaxParts; ++t) {
+      const float dm = part[t].x - mean;
+      m2 += part[t].y + (float)kLnPartW * dm * dm;
+    }
+    const float rstd = 1.0f / sqrtf(m2 * inv_k + ln.eps);
+    if (threadIdx.x < T::BM) st[(nkd.div(s) & 1) * T::BM + threadIdx.x] = make_float2(mean, rstd);
+  }
+  // at the top of the iteration that stores slice s: its rows' (mean, rstd) from LDS, read
+  // under the MFMAs
+  __device__ __forceinline__ void stage_in(int s) {
+    if constexpr (MQ_LN_DIAG == 1) return;
+    const float2* ms = st + (nkd.div(s < S ? s : S - 1) & 1) * T::BM;
+#pragma unroll
+    for (int a = 0; a < A_LOADS; ++a) mr[a] = ms[((int)threadIdx.x + a * T::THREADS) / T::F4_PER_ROW];
+  }
+  template <class DC>
+  __device__ __forceinline__ void xform(Stager<T>& sg, int s, DC) {
+    if constexpr (MQ_LN_DIAG != 0) return;
+    constexpr int d = DC::value;
+#pragma unroll
+    for (int a = 0; a < A_LOADS; ++a) sg.r[a] = (sg.r[a] - mr[a].x) * mr[a].y * gg[d] + bb[d];
+    const int sc = s < S ? s : S - 1;
+    const int i = nkd.div(sc), kt = sc - i * nk;
+    int m0;
+    int64_t n0;
+    coords(i, m0, n0);
+    if (n0 == 0 && s < S) {  // column-0 tiles: LN(A) rows out to x (workgroup-uniform)
+      const int ch = threadIdx.x % T::F4_PER_ROW;
+#pragma unroll
+      for (int a = 0; a < A_LOADS; ++a) {
+        // rows past M were staged from row M - 1 (clamped): they store row M - 1's own values
+        const int r = min(m0 + ((int)threadIdx.x + a * T::THREADS) / T::F4_PER_ROW, M - 1);
+        *reinterpret_cast<floatx4*>(ln.xout + (int64_t)r * ln.ldx + kt * T::BK + ch * 4) = sg.r[a];
+      }
+    }
+  }
+};
+
+template <class T, int EPI, bool LN_IN = false>
 __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const float* __restrict__ A, int lda,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ resid, int ldr,
                                                          float* __restrict__ out, int ldo, int M,
-                                                         int N, int K) {
+                                                         int N, int K, LnArgs ln) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
+  __shared__ float2 ln_st[LN_IN ? 2 * T::BM : 1];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
   const int tiles_n = (N + T::BN - 1) / T::BN;
@@ -101,6 +228,78 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
     int64_t n0l;
     coords(i, m0, n0l);
     const int n0 = (int)n0l;
+    if constexpr (EPI == EPI_RESID_STATS) {
+      // y = acc + bias + resid, then per row the partial (mean, M2) of y over the wave
+      // tile's WN = kLnPartW columns: the 32 lanes of a lane half hold a row's columns
+      // (tn-major), reduced by xor shuffles within the half.  Full tiles load the residual
+      // and store y by buffer ops off the wave tile's origin with scalar row offsets (as the
+      // EPI_RESID path below); a ragged last row band uses guarded plain accesses.
+      static_assert(T::WN == kLnPartW, "stats partials are per kLnPartW-column wave tile");
+      const int wr0 = m0 + wm * T::WM, wc0 = n0 + wn * T::WN;
+      const int part = wc0 / T::WN;
+      float bv[T::TN];
+#pragma unroll
+      for (int tn = 0; tn < T::TN; ++tn) bv[tn] = bias[wc0 + tn * 32 + (lane & 31)];
+      float rv[T::TM][T::TN][16];
+      const bool full = m0 + T::BM <= M;
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(out + (int64_t)wr0 * ldo + wc0), (short)0, 0x7fffffff, 0x00020000);
+      const int ol = (4 * (lane >> 5) * ldo + (lane & 31)) * 4;
+      if (full) {
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(resid + (int64_t)wr0 * ldr + wc0), (short)0, 0x7fffffff, 0x00020000);
+        const int rl = (4 * (lane >> 5) * ldr + (lane & 31)) * 4;
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              rv[tm][tn][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                  rr, rl, (acc_row(tm, e, 0) * ldr + tn * 32) * 4, 0));
+      } else {
+#pragma unroll
+        for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < T::TN; ++tn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int row = min(wr0 + acc_row(tm, e, lane), M - 1);
+              rv[tm][tn][e] = resid[(int64_t)row * ldr + wc0 + tn * 32 + (lane & 31)];
+            }
+      }
+#pragma unroll
+      for (int tm = 0; tm < T::TM; ++tm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = wr0 + acc_row(tm, e, lane);
+          float v[T::TN], sum = 0.f;
+#pragma unroll
+          for (int tn = 0; tn < T::TN; ++tn) {
+            v[tn] = acc[tm][tn][e] + bv[tn] + rv[tm][tn][e];
+            sum += v[tn];
+          }
+          if (full) {
+#pragma unroll
+            for (int tn = 0; tn < T::TN; ++tn)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[tn]), ro, ol, (acc_row(tm, e, 0) * ldo + tn * 32) * 4, 0);
+          } else if (row < M) {
+#pragma unroll
+            for (int tn = 0; tn < T::TN; ++tn) out[(int64_t)row * ldo + wc0 + tn * 32 + (lane & 31)] = v[tn];
+          }
+#pragma unroll
+          for (int off = 16; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+          const float mean = sum * (1.0f / T::WN);
+          float m2 = 0.f;
+#pragma unroll
+          for (int tn = 0; tn < T::TN; ++tn) m2 += (v[tn] - mean) * (v[tn] - mean);
+#pragma unroll
+          for (int off = 16; off > 0; off >>= 1) m2 += __shfl_xor(m2, off);
+          if ((lane & 31) == 0 && row < M)
+            reinterpret_cast<float2*>(ln.stats_out)[(int64_t)row * ln.nt + part] = make_float2(mean, m2);
+        }
+      return;
+    }
     if (m0 + T::BM <= M && n0 + T::BN <= N) {
       // full tile: every bias / residual load goes out before the first use, so the
       // tile pays one memory round trip (the guarded loop below waits per element).
@@ -161,7 +360,13 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
         }
     }
   };
-  walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
+  if constexpr (LN_IN) {
+    LnInHooks<T, decltype(coords)> hk{ln, coords, ln_st, M, K / T::BK, n_tiles * (K / T::BK), 1.0f / (float)K,
+                                      FastDiv(K / T::BK)};
+    walk_tiles_hooked<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi, hk);
+  } else {
+    walk_tiles<T>(lds, n_tiles, TileOperands{A, lda, M, W, K, N, K}, coords, epi);
+  }
 }
 
 // ------------------------------------------- K4 / K6: residual GEMM + LayerNorm ---
@@ -1417,13 +1622,13 @@ struct GemmArgs {
   int M, N, K;
 };
 
-template <class T, int EPI>
-void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s) {
+template <class T, int EPI, bool LN_IN = false>
+void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s, const LnArgs& ln = LnArgs{}) {
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
   // persistent grid: the workgroups that fit the CUs at once, a multiple of 8
   const int grid = (std::min(tiles, T::WG_PER_CU * num_cus) + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda, g.W,
-                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, LN_IN>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda, g.W,
+                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K, ln);
 }
 
 using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128
@@ -1532,6 +1737,26 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false,
   launch_gemm_tile<EPI>(g, best, num_cus, s);
 }
 
+// LayerNorm deferred into the consumer (LnArgs): the producer is the 128x96 tile (its wave
+// tile is the partial width), the consumer the 128x128 or 128x96 tile by launch_gemm's
+// waste model over those two.
+void launch_gemm_stats(const GemmArgs& g, const LnArgs& ln, int num_cus, hipStream_t s) {
+  launch_gemm_t<GemmT96, EPI_RESID_STATS>(g, num_cus, s, ln);
+}
+
+template <int EPI>
+void launch_gemm_ln_in(const GemmArgs& g, const LnArgs& ln, int num_cus, hipStream_t s) {
+  const int64_t slots = 2 * (int64_t)num_cus;
+  auto cost = [&](int bn, double eff) {
+    const int64_t tiles = (int64_t)((g.M + 127) / 128) * ((g.N + bn - 1) / bn);
+    return (double)((tiles + slots - 1) / slots) * 128 * bn / eff;
+  };
+  if (cost(128, 1.0) <= cost(96, 0.96))
+    launch_gemm_t<GemmBig, EPI, true>(g, num_cus, s, ln);
+  else
+    launch_gemm_t<GemmT96, EPI, true>(g, num_cus, s, ln);
+}
+
 // Stage labels for the optional per-kernel-class event timeline.
 enum Stage { ST_EMBED = 0, ST_QKV, ST_ATTN, ST_OPROJ, ST_LN, ST_FFN_UP, ST_FFN_DOWN, ST_POOL, ST_N };
 
@@ -1546,7 +1771,7 @@ struct mq_encoder {
   Buf weights;
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
-  Buf x, y, qkv, ctx, ffn, io_out, slab;
+  Buf x, y, qkv, ctx, ffn, io_out, slab;  // (+ lnst below)
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -1570,6 +1795,9 @@ struct mq_encoder {
   int ln_rows_per_wave = 4;     // batched LayerNorm kernel: rows per wave
   bool fused_ln = false;        // batched residual GEMMs: LayerNorm in the epilogue (full-row tiles;
                                 // measured slower, kept as an option: DESIGN.md §4)
+  bool ln_on_load = false;      // batched forward: LayerNorm applied by the consuming GEMM (LnArgs;
+                                // measured slower: the consumers' staging VALU)
+  Buf lnst;                     // its per-row partials, two sets of [M][H / kLnPartW] (mean, M2)
   bool use_graphs = false;  // eager measured faster for one query (0.628 vs 0.645 ms: the
                             // graph path stages ids / mask / out through its own buffers)
   uint64_t graph_clock = 0;
@@ -1647,38 +1875,95 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
   e->tl.mark(s, ST_EMBED);
   hipLaunchKernelGGL((embed_ln_kernel<VPL>), dim3(row_blocks), dim3(256), 0, s, ids, M, L,
                      c.vocab_size, e->word, e->pos, e->typ, e->eg, e->eb, c.ln_eps, e->x.p);
+  // LayerNorm deferred into the consumers (LnArgs) on the full-M layers: exact f32, rows
+  // enough for the tiled path, hidden a whole number of kLnPartW-column partials
+  const int nt = H / kLnPartW;
+  const bool lnl = e->ln_on_load && !e->fused_ln && e->precision == MQ_DTYPE_F32 && M > 256 &&
+                   H == kLnPartW * kLnMaxParts && e->lnst.n >= (size_t)4 * M * nt;
+  float* st1 = e->lnst.p;                          // out-proj -> FFN-up
+  float* st2 = lnl ? e->lnst.p + (size_t)2 * M * nt : nullptr;  // FFN-down -> next QKV
+  bool y_pending = false;  // x holds LN2's input y (+ st2) instead of the LayerNorm output
+  const LayerW* prev = nullptr;
+  auto ln_args = [&](const float* stats, const float* g, const float* b) {
+    LnArgs a{};
+    a.stats_in = stats;
+    a.g = g;
+    a.b = b;
+    a.xout = e->x.p;
+    a.ldx = H;
+    a.nt = nt;
+    a.eps = c.ln_eps;
+    return a;
+  };
+  auto stats_out = [&](float* stats) {
+    LnArgs a{};
+    a.stats_out = stats;
+    a.nt = nt;
+    return a;
+  };
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
     const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
     // rows this layer carries past attention: all M tokens, or the B CLS rows
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;  // row stride of x / ctx views
+    // QKV input: x, or (deferred LN2 of the previous layer) y normalised while staged,
+    // the column-0 tiles writing LN2(y) to x for the residual and the CLS-row Q GEMM
+    const float* qkv_in = y_pending ? e->y.p : e->x.p;
+    auto qkv_gemm = [&](const GemmArgs& g) {
+      if (y_pending) {
+        e->tl.mark(s, ST_QKV);
+        launch_gemm_ln_in<EPI_BIAS>(g, ln_args(st2, prev->ln2g, prev->ln2b), e->num_cus, s);
+      } else {
+        gemm<EPI_BIAS>(e, g, ST_QKV, s);
+      }
+    };
     if (cls_only && L > 1) {
       // only the CLS rows need queries: K and V for every token ([M, 2H] into qkv columns
       // H..3H), Q for the B CLS rows (every L-th row of x into row b*L of qkv)
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0,
-                         e->qkv.p + H, 3 * H, M, 2 * H, H},
-                     ST_QKV, s);
+      qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0, e->qkv.p + H,
+                3 * H, M, 2 * H, H});
       gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, L * H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, L * 3 * H,
                          B, H, H},
                      ST_QKV, s);
     } else {
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H},
-                     ST_QKV, s);
+      qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H});
     }
+    y_pending = false;
     e->tl.mark(s, ST_ATTN);
     const int qt = cls_only ? 1 : q_tiles;
     launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
-    // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y)
-    gemm_resid_ln<VPL>(e, {e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H},
-                       w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
-    const GemmArgs up{e->slab.p, e->slab.n, e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F, rows, F, H};
-    if (c.gelu == MQ_GELU_TANH)
+    const bool lnl_layer = lnl && !cls_only;
+    // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y) - or, deferred, y + partials
+    const GemmArgs oproj{e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H};
+    if (lnl_layer) {
+      e->tl.mark(s, ST_OPROJ);
+      launch_gemm_stats(oproj, stats_out(st1), e->num_cus, s);
+    } else {
+      gemm_resid_ln<VPL>(e, oproj, w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
+    }
+    const GemmArgs up{e->slab.p, e->slab.n, lnl_layer ? e->y.p : e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F,
+                      rows, F, H};
+    if (lnl_layer) {  // FFN-up normalises y (LN1) while staging; its column-0 tiles write x
+      e->tl.mark(s, ST_FFN_UP);
+      if (c.gelu == MQ_GELU_TANH)
+        launch_gemm_ln_in<EPI_GELU_TANH>(up, ln_args(st1, w.ln1g, w.ln1b), e->num_cus, s);
+      else
+        launch_gemm_ln_in<EPI_GELU_ERF>(up, ln_args(st1, w.ln1g, w.ln1b), e->num_cus, s);
+    } else if (c.gelu == MQ_GELU_TANH) {
       gemm<EPI_GELU_TANH>(e, up, ST_FFN_UP, s);
-    else
+    } else {
       gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
-    gemm_resid_ln<VPL>(e, {e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F},
-                       w.ln2g, w.ln2b, e->x.p, ST_FFN_DOWN, s);
+    }
+    const GemmArgs down{e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F};
+    if (lnl_layer && li + 1 < e->layers.size()) {  // LN2 deferred into the next layer's QKV
+      e->tl.mark(s, ST_FFN_DOWN);
+      launch_gemm_stats(down, stats_out(st2), e->num_cus, s);
+      y_pending = true;
+    } else {
+      gemm_resid_ln<VPL>(e, down, w.ln2g, w.ln2b, e->x.p, ST_FFN_DOWN, s);
+    }
+    prev = &w;
   }
   e->tl.mark(s, ST_POOL);
   const bool pruned = c.pooling == MQ_POOL_CLS;  // x holds [B, H] CLS rows
@@ -2170,6 +2455,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value == 0 || value == 1, "fused_ln must be 0 or 1 (got %d)", value);
       e->fused_ln = value != 0;
       break;
+    case MQ_ENC_OPT_LN_ON_LOAD:
+      MQ_CHECK_ARG(value == 0 || value == 1, "ln_on_load must be 0 or 1 (got %d)", value);
+      e->ln_on_load = value != 0;
+      break;
     case MQ_ENC_OPT_SPLITK_TILES:
       MQ_CHECK_ARG(value >= 0 && value <= 4096, "splitk_tiles must be in [0, 4096] (got %d)", value);
       e->splitk_tiles = value;
@@ -2193,6 +2482,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_LN_ROWS_PER_WAVE: *value = e->ln_rows_per_wave; break;
     case MQ_ENC_OPT_FUSE_ATTN_OPROJ: *value = e->fuse_attn_oproj ? 1 : 0; break;
     case MQ_ENC_OPT_FUSED_LN: *value = e->fused_ln ? 1 : 0; break;
+    case MQ_ENC_OPT_LN_ON_LOAD: *value = e->ln_on_load ? 1 : 0; break;
     case MQ_ENC_OPT_SPLITK_TILES: *value = e->splitk_tiles; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
@@ -2239,9 +2529,10 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   rc = e->slab.ensure((size_t)2 * e->num_cus * 32 * 128);
   if (rc) return rc;
   // y also holds the few-row forward's output-projection planes (<= 4 of M rows)
+  const size_t ln_parts = e->ln_on_load && M > 256 ? (size_t)4 * M * std::max(1, c.hidden / kLnPartW) : 0;
   for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, (M <= (size_t)kRowsMax ? 4 : 1) * M * c.hidden),
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
-                  std::make_pair(&e->ffn, M * c.ffn)}) {
+                  std::make_pair(&e->ffn, M * c.ffn), std::make_pair(&e->lnst, ln_parts)}) {
     rc = bn.first->ensure(bn.second);
     if (rc) return rc;
   }

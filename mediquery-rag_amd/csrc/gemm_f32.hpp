@@ -407,3 +407,83 @@ __device__ __forceinline__ void walk_tiles(float* lds, int n_tiles, const TileOp
 }
 
 }  // namespace mq
+
+namespace mq {
+
+// walk_tiles with hooks around the operand staging (D >= 2), for GEMMs that transform an
+// operand between its global load and its LDS write (LayerNorm on load, encoder.hip):
+//   hk.issue(s, IC<d>)      before the loads of slice s (unclamped; s >= S: the re-read
+//                           past the end) into register stage d
+//   hk.prepare(s)           at the store phase of the iteration that fetched slice s, before
+//                           that iteration's barrier (per-tile state into LDS: read by
+//                           xform from the next iteration on)
+//   hk.stage_in(s)          at the top of the iteration that stores slice s (before its
+//                           MFMAs: per-slice state read from LDS under them)
+//   hk.xform(st, s, IC<d>)  on stage d's registers just before they are written to LDS
+// Otherwise the slice schedule is walk_tiles' (same loads, MFMAs, barriers).
+template <class T, int D = T::PF, class Coords, class Epi, class Hooks>
+__device__ __forceinline__ void walk_tiles_hooked(float* lds, int n_tiles, const TileOperands& op,
+                                                  Coords coords, Epi epi, Hooks& hk) {
+  static_assert(D >= 2, "the hooks need the slice's loads one iteration before its store");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
+  const int nk = op.K / T::BK;
+  const int S = n_tiles * nk;
+  if (S == 0) return;
+  const FastDiv nkd(nk);
+  auto fetch = [&](Stager<T>& st, int j) {
+    const int i = nkd.div(j), kt = j - i * nk;
+    int m0;
+    int64_t n0;
+    coords(i, m0, n0);
+    // tile origins are workgroup-uniform: keep them (and the buffer descriptors built from
+    // them) scalar whatever the hooks' per-thread code does to the uniformity analysis
+    m0 = __builtin_amdgcn_readfirstlane(m0);
+    n0 = (int64_t)__builtin_amdgcn_readfirstlane((int)n0);
+    st.load(op.A, op.lda, op.M, m0, op.B, op.ldb, op.N, n0, kt * T::BK, tid);
+  };
+  floatx16 acc[T::TM][T::TN];
+  Stager<T> st[D];
+  static_for<D>([&](auto dc) {
+    constexpr int d = decltype(dc)::value;
+    hk.issue(d, dc);
+    fetch(st[d], d < S ? d : S - 1);
+  });
+  static_for<D>([&](auto dc) { hk.prepare(decltype(dc)::value); });
+  __syncthreads();
+  hk.stage_in(0);
+  hk.xform(st[0], 0, IC<0>{});
+  st[0].store(lds, tid);
+  zero_acc<T>(acc);
+  __syncthreads();
+  for (int j0 = 0; j0 < S; j0 += D) {
+    bool done = false;
+    static_for<D>([&](auto dc) {
+      constexpr int d = decltype(dc)::value;
+      const int j = j0 + d;
+      if (done || j >= S) {
+        done = true;
+        return;
+      }
+      hk.issue(j + D, dc);
+      fetch(st[d], min(j + D, S - 1));
+      hk.stage_in(j + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      float* cur = lds + (j & 1) * T::STAGE_FLOATS;
+      __builtin_amdgcn_s_setprio(1);
+      mma_slice<T>(cur, acc, wm, wn, lane);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      hk.prepare(j + D);
+      hk.xform(st[(d + 1) % D], j + 1, IC<(d + 1) % D>{});
+      st[(d + 1) % D].store(lds + ((j + 1) & 1) * T::STAGE_FLOATS, tid);
+      __syncthreads();
+      if (nkd.mod(j + 1) == 0) {
+        epi(nkd.div(j), acc, cur);
+        zero_acc<T>(acc);
+      }
+    });
+  }
+}
+
+}  // namespace mq

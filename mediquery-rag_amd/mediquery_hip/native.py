@@ -233,11 +233,11 @@ class Encoder:
     OPTIONS = {"rows_max": _lib.MQ_ENC_OPT_ROWS_MAX, "rows_splits": _lib.MQ_ENC_OPT_ROWS_SPLITS,
                "splitk_max": _lib.MQ_ENC_OPT_SPLITK_MAX, "ln_rows_per_wave": _lib.MQ_ENC_OPT_LN_ROWS_PER_WAVE,
                "fuse_attn_oproj": _lib.MQ_ENC_OPT_FUSE_ATTN_OPROJ, "fused_ln": _lib.MQ_ENC_OPT_FUSED_LN,
-               "splitk_tiles": _lib.MQ_ENC_OPT_SPLITK_TILES}
+               "splitk_tiles": _lib.MQ_ENC_OPT_SPLITK_TILES, "ln_on_load": _lib.MQ_ENC_OPT_LN_ON_LOAD}
 
     def set_option(self, name, value):
         """Tuning option of the forward (mq_encoder_set_option): rows_max, rows_splits,
-        splitk_max, ln_rows_per_wave, fuse_attn_oproj, fused_ln."""
+        splitk_max, ln_rows_per_wave, fuse_attn_oproj, fused_ln, splitk_tiles, ln_on_load."""
         _lib.call("mq_encoder_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name):

@@ -42,6 +42,40 @@ def test_golden(require_gpu, g, case, cfg, prec):
     _close(enc.embed(g[src + "_ids"], g[src + "_mask"]), g[case + "_emb"])
 
 
+@pytest.mark.parametrize("B,L,layers,pool,gelu", [
+    (9, 33, 3, POOL_MEAN, None),    # 297 rows: ragged 128-row tiles, the last layer's LN2 on its own
+    (9, 33, 3, None, GELU_TANH),    # CLS pooling: the cls-only last layer's K/V GEMM normalises on load
+    (5, 200, 2, None, None),        # 1000 rows, long sequences
+    (300, 3, 4, POOL_MEAN, None),   # many short sequences
+])
+def test_layernorm_on_load_vs_oracle(require_gpu, B, L, layers, pool, gelu):
+    """LayerNorm deferred into the consuming GEMM (MQ_ENC_OPT_LN_ON_LOAD = 1; measured
+    slower, off by default): out-proj / FFN-down leave per-row partials, FFN-up / the next
+    QKV normalise A while staging and their column-0 tiles write the residual x.  Against
+    the oracle, and against the LayerNorm-launch path of the same encoder within 1e-5 (two
+    summation orders of the same statistics)."""
+    kw = {"layers": layers}
+    if pool is not None:
+        kw["pooling"] = pool
+    if gelu is not None:
+        kw["gelu"] = gelu
+    cfg = BertConfig(**kw)
+    rng = np.random.default_rng(B * 7 + L)
+    ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    for b in range(0, B, 2):
+        n = int(rng.integers(1, L + 1))
+        mask[b, n:] = 0
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    enc = Encoder(cfg)
+    assert enc.get_option("ln_on_load") == 0
+    base = enc.embed(ids, mask)
+    enc.set_option("ln_on_load", 1)
+    got = enc.embed(ids, mask)
+    _close(got, ref)
+    np.testing.assert_allclose(got, base, atol=1e-5, rtol=0)
+
+
 @pytest.mark.parametrize("prec", [_lib.MQ_DTYPE_F32, _lib.MQ_DTYPE_F32X6])
 def test_headline_shape_vs_oracle(require_gpu, prec):
     """The exact encoder shape bench.py times (BASELINE config 3; the query embedding of
@@ -205,6 +239,7 @@ def test_errors(require_gpu):
     ("fuse_attn_oproj", 0, 1, 32), ("fuse_attn_oproj", 0, 2, 17),
     ("fused_ln", 1, 70, 32), ("fused_ln", 1, 9, 130),
     ("splitk_tiles", 64, 1, 256), ("splitk_tiles", 4096, 1, 100), ("splitk_tiles", 16, 2, 48),
+    ("ln_on_load", 1, 70, 32), ("ln_on_load", 1, 9, 130),
 ])
 def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     """Every non-default value of the explicit tuning options (mq_encoder_set_option,
