@@ -758,6 +758,17 @@ __device__ long long mq_ktrace[kTraceRegions * kTraceWgs * kTraceSlots];
   do {                         \
   } while (0)
 #endif
+// Measurement builds with -DMQ_ROWS_REPEAT: every few-row launch runs twice back to back
+// (all five are idempotent), so a kernel trace shows each launch cold and with its
+// weights warm in L2 / MALL - what a next-phase weight prefetch could at best recover.
+#if defined(MQ_ROWS_REPEAT) && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_ROWS_REPEAT is a measurement build option (-DMQ_MEASUREMENT_BUILD)"
+#endif
+#ifdef MQ_ROWS_REPEAT
+#define ROWS_REP for (int rep_ = 0; rep_ < 2; ++rep_)
+#else
+#define ROWS_REP
+#endif
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
 constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
@@ -2142,10 +2153,10 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       g0.vocab = c.vocab_size;
       g0.pos = e->pos;
       g0.typ = e->typ;
-      launch_rows_ln<EPI_BIAS, VPL>(g0, 0, e->eg, e->eb, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(g0, 0, e->eg, e->eb, eps, e->x.p, s);
     } else {
       const LayerW& p = e->layers[li - 1];
-      launch_rows_ln<EPI_BIAS, VPL>({e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p,
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>({e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p,
                                      3 * H, 0, M, 3 * H, H, 1},
                                     dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
     }
@@ -2156,7 +2167,7 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       const int rps = cls_only ? 1 : L, qtiles = (rps + 15) / 16;
       y_planes = c.heads / hg;
       const dim3 grid(H / kOpCols, B * qtiles, y_planes);
-      launch_attn_oproj(hg, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wo, w.bo, e->x.p,
+      ROWS_REP launch_attn_oproj(hg, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wo, w.bo, e->x.p,
                         stride, e->y.p, (int64_t)rows * H);
     } else {
       e->tl.mark(s, ST_ATTN);
@@ -2171,11 +2182,11 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     e->tl.mark(s, ST_FFN_UP);
     const RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
     if (c.gelu == MQ_GELU_TANH)
-      launch_rows_ln<EPI_GELU_TANH, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_GELU_TANH, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     else
-      launch_rows_ln<EPI_GELU_ERF, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_GELU_ERF, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     e->tl.mark(s, ST_FFN_DOWN);
-    launch_rows<EPI_RESID>({e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F,
+    ROWS_REP launch_rows<EPI_RESID>({e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F,
                             dsplit},
                            s);
     prev_rows = rows;
