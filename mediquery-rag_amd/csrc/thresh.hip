@@ -99,7 +99,8 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       qf[c * 4 + s] = __builtin_bit_cast(bf16x8, Qb[(int64_t)q * (NCH * 8) + c * 8 + 2 * s + h]);
-  float t = MODE == TS_APPEND ? tau[q] : 0.f;
+  // (measurement builds that replace operands score garbage: no row may clear tau there)
+  float t = MODE == TS_APPEND ? (MQ_TS_DBG & 6 ? INFINITY : tau[q]) : 0.f;
   // Retire the fragment loads here, visibly to the compiler: every later use reads the
   // asm's outputs, so no wait for these loads lands in the loop, where the (invisible)
   // DMAs of the ring would make any counted vmcnt drain the prefetch.
