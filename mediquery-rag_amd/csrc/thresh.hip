@@ -165,10 +165,15 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
     a[0] = frag(0);
     a[1] = frag(1);
     a[2] = frag(2);
+    // block i+2's source and ring slot, once per block (not per DMA slot)
+    const unsigned char* nsrc = C + (first + (int64_t)min(i + 2, nb - 1) * stride) * BLK_B;
+    const unsigned nlds = ring_lds + ((i + 2) % kTsBufs) * BLK_B;
     static_for<NCH * 4>([&](auto sc) {
       constexpr int st = decltype(sc)::value;
-      if constexpr (st % 8 == 0 && st / 8 < DMA_PER_WAVE && !(MQ_TS_DBG & 2))
-        issue_one(i + 2, (i + 2) % kTsBufs, st / 8);
+      if constexpr (st % 8 == 0 && st / 8 < DMA_PER_WAVE && !(MQ_TS_DBG & 2)) {
+        const int d = wave * DMA_PER_WAVE + st / 8;
+        glds16(nsrc, dofs[d & 1] + (unsigned)((d & 3) * 8 * ROW_B + (d >> 2) * 128), nlds + d * 1024);
+      }
       if constexpr (st + 3 < NCH * 4) a[(st + 3) & 3] = (MQ_TS_DBG & 4) ? qf[(st + 5) % (NCH * 4)] : frag(st + 3);
       __builtin_amdgcn_sched_barrier(0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[st & 3], qf[st], acc, 0, 0, 0);
