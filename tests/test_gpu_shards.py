@@ -183,3 +183,73 @@ def test_two_process_hip_shards_single_allgather(require_gpu):
         assert check_topk(ids, scores, ref, K) == []
         np.testing.assert_array_equal(ids_dp, ids[rank * half:(rank + 1) * half])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def _rccl_worker(port, out_q, N, K, NQ):
+    """One rank on the RCCL backend: the exact calls bench.py makes at N > 1
+    (init_process_group("nccl", device_id=...), the packed candidate all-gather, the query
+    all-gather and the batch-size all-gather of device tensors), at world size 1 - RCCL
+    needs one GPU per rank, so more ranks cannot share this box's single GPU."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "mediquery-rag_amd"), root]
+    import torch
+    import torch.distributed as dist
+    from mediquery_hip import synth as sy
+    from mediquery_hip.distributed import ShardedSearcher
+    from mediquery_hip.native import FlatIndex as FI
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        c = sy.corpus(N, 768, clustered=True)
+        ix = FI(dim=768, device=0)
+        ix.add_device(torch.from_numpy(c).to(dev))
+        s_loc = torch.empty((NQ, K), dtype=torch.float32, device=dev)
+        i_loc = torch.empty((NQ, K), dtype=torch.int64, device=dev)
+
+        def local(qq, k):
+            ix.search_device(qq, k, s_loc[:qq.shape[0]], i_loc[:qq.shape[0]])
+            return s_loc[:qq.shape[0]], i_loc[:qq.shape[0]]
+
+        q, _ = sy.queries(NQ, c)
+        qd = torch.from_numpy(q).to(dev)
+        ss = ShardedSearcher(local, 0)
+        s, i = ss.search(qd, K)
+        g = ss.gather_queries(qd)
+        _, i2 = ss.search_local_batch(qd[:NQ - 3], K)  # sizes=None: the size all-gather runs
+        ix.search_device(qd, K, s_loc, i_loc)
+        torch.cuda.synchronize()
+        out_q.put((s.is_cuda, i.cpu().numpy(), s.cpu().numpy(), bool(torch.equal(g, qd)), i2.cpu().numpy(),
+                   i_loc.cpu().numpy()))
+    except Exception as e:  # report instead of leaving the parent waiting
+        out_q.put((repr(e),))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_backend_exchange_world1(require_gpu):
+    """The RCCL code path of the sharded search (device tensors through
+    all_gather_into_tensor on the nccl backend), checked against the plain index."""
+    import torch.multiprocessing as mp
+    N, K, NQ = 20011, 5, 48
+    ctx = mp.get_context("spawn")
+    q_out = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q_out, N, K, NQ))
+    p.start()
+    try:
+        r = q_out.get(timeout=100)
+    finally:
+        p.join(timeout=30)
+    assert len(r) > 1, r[0]
+    assert p.exitcode == 0
+    on_device, ids, scores, gathered_ok, ids_b, ids_plain = r
+    assert on_device and gathered_ok
+    np.testing.assert_array_equal(ids, ids_plain)
+    np.testing.assert_array_equal(ids_b, ids_plain[:NQ - 3])
+    c = synth.corpus(N, 768, clustered=True)
+    q, _ = synth.queries(NQ, c)
+    assert check_topk(ids, scores, exact_scores(q, c), K) == []
