@@ -539,13 +539,14 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
+constexpr int kFinW = 8, kFinT = 64 * kFinW;  // K9q finish: 8 waves, all 64 re-rank gathers in one round
 // K9q finish, one block per query (the single-query int8 screen, fused to save launches
 // on the latency path): the survivors' top-kc by screen score (as bf16_select_kernel:
 // slots past the survivors hold (tau, -1), more than kTsCap survivors -> bound +inf),
 // the exact fp32 re-rank of the prefix that can still reach the top-k (screen >=
 // s_k - 2E, as rerank_kernel), the top-k by (score desc, id asc), and the certificate
 // s_kc + E < e_k (as screen_verify_kernel, mode VERIFY_BF16_Q32 with the int8 maxima).
-__global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict__ Q,
+__global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restrict__ Q,
                                                         const float* __restrict__ rows, int dim,
                                                         const float* __restrict__ ts_cs,
                                                         const int* __restrict__ ts_ci,
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int total = count[q];
   const int cnt = min(total, kTsCap);
-  for (int i = tid; i < cnt; i += 256) {
+  for (int i = tid; i < cnt; i += kFinT) {
     ls[i] = ts_cs[q * kTsCap + i];
     li[i] = ts_ci[q * kTsCap + i];
   }
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict_
     }
   }
   __syncthreads();
-  for (int i = tid; i < cnt; i += 256) {
+  for (int i = tid; i < cnt; i += kFinT) {
     const float x = ls[i];
     const int xi = li[i];
     int rank = 0;
@@ -607,9 +608,9 @@ __global__ __launch_bounds__(256) void i8_finish_kernel(const float* __restrict_
   __syncthreads();
   const int kl = live_sh;
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
-  constexpr int U = 8;  // eight candidates per wave per round (rerank_kernel's arithmetic)
+  constexpr int U = 8;  // eight candidates per wave per round (rerank_kernel's arithmetic): 64 per round
   const int slot = rerank_slot(lane);
-  for (int c0 = wave * U; c0 < kl; c0 += 4 * U) {
+  for (int c0 = wave * U; c0 < kl; c0 += kFinW * U) {
     long long id[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) id[u] = c0 + u < kl ? ci[c0 + u] : -1;
@@ -1689,7 +1690,7 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     // shadow's maxima (kc = 64 < n: the int8 tier needs >= kTsMinRows rows)
     rc = i8_topk(ix, q, nq, kc, nullptr, nullptr, s, ix->flag.as<int>());
     if (rc) return rc;
-    hipLaunchKernelGGL(i8_finish_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+    hipLaunchKernelGGL(i8_finish_kernel, dim3((unsigned)nq), dim3(kFinT), 0, s, q, ix->rows, ix->dim,
                        ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
                        kc, k, ix->stats8.as<unsigned>(), os, oi, ix->flag.as<int>(), fail);
     ix->tl.close(s);
