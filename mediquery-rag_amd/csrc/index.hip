@@ -539,6 +539,12 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
+#ifndef MQ_FIN_DBG  // measurement builds only (wrong results): 1 = no survivor ranking, 2 = no re-rank gathers
+#define MQ_FIN_DBG 0
+#endif
+#if MQ_FIN_DBG != 0 && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_FIN_DBG computes wrong results: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
+#endif
 constexpr int kFinW = 8, kFinT = 64 * kFinW;  // K9q finish: 8 waves, all 64 re-rank gathers in one round
 // K9q finish, one block per query (the single-query int8 screen, fused to save launches
 // on the latency path): the survivors' top-kc by screen score (as bf16_select_kernel:
@@ -588,6 +594,13 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
   for (int i = tid; i < cnt; i += kFinT) {
     const float x = ls[i];
     const int xi = li[i];
+    if (MQ_FIN_DBG & 1) {
+      if (i < kc) {
+        cs[i] = x;
+        ci[i] = xi;
+      }
+      continue;
+    }
     int rank = 0;
 #pragma unroll 8
     for (int j = 0; j < cnt; ++j) rank += better(ls[j], li[j], x, xi) ? 1 : 0;
@@ -614,7 +627,7 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
     long long id[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) id[u] = c0 + u < kl ? ci[c0 + u] : -1;
-    const float dot = rerank_dots8(q4, rows, dim, id, lane);
+    const float dot = (MQ_FIN_DBG & 2) ? 0.f : rerank_dots8(q4, rows, dim, id, lane);
     long long my_id = id[0];
 #pragma unroll
     for (int u = 1; u < U; ++u) my_id = slot == u ? id[u] : my_id;
