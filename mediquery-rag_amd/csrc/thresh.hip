@@ -59,11 +59,17 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // ring's prefetch each block.  Completion is counted by hand (s_waitcnt vmcnt(N)).  The
 // SGPR-base form keeps one 32-bit VGPR per address (the kernel runs at ~240 VGPRs: a
 // spill reload inside the loop would wait vmcnt(0) and serialise the ring).
+#ifndef MQ_TS_NT  // 1: the ring's row stream is non-temporal.  Measured (r4): -2% at one query group
+#define MQ_TS_NT 0    // (B <= 256), +4% at four (B = 1024: the groups re-read the rows), so off
+#endif
 __device__ __forceinline__ void glds16(const void* base, unsigned voff, unsigned lds_dst) {
   unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+#if MQ_TS_NT
+      " nt"
+#endif
+      "\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
       : "memory");
@@ -424,6 +430,9 @@ __device__ __forceinline__ float key_ord(unsigned k) {
 #ifndef MQ_I8_ROWS
 #define MQ_I8_ROWS 8
 #endif
+#ifndef MQ_I8_NT  // 1: the int8 shadow streams with non-temporal loads (read once per search)
+#define MQ_I8_NT 1
+#endif
 constexpr int kI8Rows = MQ_I8_ROWS;  // rows per wave step (8 or 16)
 #ifndef MQ_I8_STAGES
 #define MQ_I8_STAGES 3
@@ -485,7 +494,7 @@ __device__ __forceinline__ void i8_load(const unsigned* __restrict__ r8, int64_t
   for (int r = 0; r < kI8Rows; ++r) {
     const unsigned* p = r8 + (unit * kI8Rows + r) * DIM4 + lane * E4;
 #pragma unroll
-    for (int d = 0; d < E4; ++d) a[r][d] = p[d];
+    for (int d = 0; d < E4; ++d) a[r][d] = MQ_I8_NT ? __builtin_nontemporal_load(p + d) : p[d];
   }
 }
 
