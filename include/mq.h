@@ -230,6 +230,12 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *                                input, from per-row partials the residual GEMM leaves (1), or
  *                                a LayerNorm launch each (0, default: the staging VALU cost the
  *                                QKV / FFN-up GEMMs 16-18%, more than the 24 launches save)
+ *   MQ_ENC_OPT_RESIDENT_LAYERS   few-row forward: layers [0, value) load their weights with
+ *                                the default cache policy, later layers non-temporally, so
+ *                                back-to-back single queries keep the first layers' weights
+ *                                in MALL (0..1024, default 8: BERT-base single query
+ *                                0.446 -> 0.427 ms encoder p50; 0 = all non-temporal is the
+ *                                slowest, 0.463)
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
@@ -239,6 +245,7 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 #define MQ_ENC_OPT_FUSED_LN 5
 #define MQ_ENC_OPT_SPLITK_TILES 6
 #define MQ_ENC_OPT_LN_ON_LOAD 7
+#define MQ_ENC_OPT_RESIDENT_LAYERS 8
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);

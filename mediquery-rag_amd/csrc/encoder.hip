@@ -769,6 +769,20 @@ __device__ long long mq_ktrace[kTraceRegions * kTraceWgs * kTraceSlots];
 #else
 #define ROWS_REP
 #endif
+// A weight fragment of the few-row kernels: default cache policy, or non-temporal for the
+// layers past the handle's `resident_layers` (MQ_ENC_OPT_RESIDENT_LAYERS), so that
+// back-to-back single queries keep the first layers' weights in the 256 MB MALL instead
+// of cycling all 340 MB through it (a cyclic sweep larger than the cache hits nothing).
+// Buffer loads off the matrix base (byte offsets < 2^31): the policy is an immediate of the
+// intrinsic, so the two forms stay two instructions (a plain load and a nontemporal-hinted
+// one under a runtime branch get merged into one plain load).
+__device__ __forceinline__ floatx4 load_w(__amdgpu_buffer_rsrc_t w, int byte_off, int nt) {
+  return __builtin_bit_cast(floatx4, nt ? __builtin_amdgcn_raw_buffer_load_b128(w, byte_off, 0, 2)
+                                        : __builtin_amdgcn_raw_buffer_load_b128(w, byte_off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const float* W) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0x7fffffff, 0x00020000);
+}
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
 constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
@@ -781,7 +795,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ W, int ldw, const float* __restrict__ bias,
     const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane,
     const int* __restrict__ ids, int L, int vocab, const float* __restrict__ pos,
-    const float* __restrict__ typ) {
+    const float* __restrict__ typ, int nt_w) {
   constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
   // 16-deep blocks per load batch: all of them while the operands fit the 128 VGPRs of a
   // 1024-thread workgroup (one memory round trip), else batches
@@ -799,7 +813,8 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   const int n0 = blockIdx.x * kRT, r0 = blockIdx.y * kRT * RT;
   const int kb0 = wave * (K / kRWaves);  // this wave's K range
   const int ks = blockIdx.z;  // K split: columns [ks K, (ks + 1) K) of A and W
-  const float* wrow = W + (int64_t)(n0 + c) * ldw + ks * K + kb0 + 4 * kq;
+  const __amdgpu_buffer_rsrc_t wr = w_rsrc(W);
+  const int wo4 = ((n0 + c) * ldw + ks * K + kb0 + 4 * kq) * 4;  // this lane's weight bytes
 
   KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 0);
   floatx4 wv[CH], av[RT][CH];
@@ -808,7 +823,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   // fragment: the launch streams W once.
 #pragma unroll
   for (int j = 0; j < CH; ++j)
-    wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+    wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : load_w(wr, wo4 + 64 * j, nt_w);
   // Everything else this launch reads from memory goes out now too, under the weight
   // loads: the epilogue's bias / residual element (thread t < 256 RT finishes element
   // t % 256 of row tile t / 256) and the LayerNorm's gamma / beta.  Loaded where they are
@@ -900,7 +915,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   for (int b = 0; b < NB; b += CH) {
     if (b > 0) {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * (b + j));
+      for (int j = 0; j < CH; ++j) wv[j] = load_w(wr, wo4 + 64 * (b + j), nt_w);
     }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -1328,7 +1343,7 @@ template <int HG, int NKB>
 __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
     const float* __restrict__ qkv, const int* __restrict__ mask, int L, int H, int rps, int qtiles,
     float scale, const float* __restrict__ Wo, const float* __restrict__ bo,
-    const float* __restrict__ resid, int ldr, float* __restrict__ out, int64_t o_plane) {
+    const float* __restrict__ resid, int ldr, float* __restrict__ out, int64_t o_plane, int nt_w) {
   // NKB = ceil(L / 16) key blocks (compile time: every operand load below is issued before
   // the first MFMA, one memory round trip for the whole launch)
   constexpr int KG = HG * kDh;     // K depth of this group's slice of the projection
@@ -1351,9 +1366,10 @@ __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
   const int cb = w & 1, kqr = w >> 1;
   floatx4 wv[NJ];
   {
-    const float* wrow = Wo + (int64_t)(n0 + cb * 16 + c) * H + h0 * kDh + kqr * KQ + 4 * g;
+    const __amdgpu_buffer_rsrc_t wr = w_rsrc(Wo);
+    const int wo4 = ((n0 + cb * 16 + c) * H + h0 * kDh + kqr * KQ + 4 * g) * 4;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const floatx4*>(wrow + 16 * j);
+    for (int j = 0; j < NJ; ++j) wv[j] = load_w(wr, wo4 + 64 * j, nt_w);
   }
   // epilogue element of threads < 512: column block et >> 8, row (et & 255) / 16
   const int et = threadIdx.x, ecb = et >> 8, erow_t = (et & 255) >> 4, ecol = n0 + ecb * 16 + (et & 15);
@@ -1806,6 +1822,9 @@ struct mq_encoder {
   int ln_rows_per_wave = 4;     // batched LayerNorm kernel: rows per wave
   bool fused_ln = false;        // batched residual GEMMs: LayerNorm in the epilogue (full-row tiles;
                                 // measured slower, kept as an option: DESIGN.md §4)
+  int resident_layers = 8;      // few-row forward: layers whose weights load with the default
+                                // cache policy (8 x 28 MB of BERT-base fit the 256 MB MALL);
+                                // later layers' loads are non-temporal
   bool ln_on_load = false;      // batched forward: LayerNorm applied by the consuming GEMM (LnArgs;
                                 // measured slower: the consumers' staging VALU)
   Buf lnst;                     // its per-row partials, two sets of [M][H / kLnPartW] (mean, M2)
@@ -2005,6 +2024,7 @@ struct RowsArgs {
   int L = 1, vocab = 0;
   const float* pos = nullptr;
   const float* typ = nullptr;
+  int nt_w = 0;  // weights loaded non-temporally (layers past resident_layers)
 };
 
 // Row tiles per workgroup: two for the LayerNorm-input GEMMs when M > 16 (the launch then
@@ -2018,7 +2038,7 @@ void launch_rows_rt(const RowsArgs& g, const float* lng, const float* lnb, float
   hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN, RT>),
                      dim3(g.N / kRT, (g.M + kRT * RT - 1) / (kRT * RT), g.splits), dim3(64 * kRWaves), 0, s,
                      g.A, g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
-                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ);
+                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ, g.nt_w);
 }
 
 template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
@@ -2086,10 +2106,10 @@ void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* 
 template <int HG>
 void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
                           int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
-                          int ldr, float* out, int64_t o_plane) {
+                          int ldr, float* out, int64_t o_plane, int nt_w) {
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(512), 0, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out,
-                       o_plane);
+                       o_plane, nt_w);
   };
   switch (nkb) {
     case 1: go(attn_oproj_rows_kernel<HG, 1>); break;
@@ -2101,11 +2121,13 @@ void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, c
 
 void launch_attn_oproj(int hg, int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
                        int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid, int ldr,
-                       float* out, int64_t o_plane) {
+                       float* out, int64_t o_plane, int nt_w) {
   if (hg == 6)
-    launch_attn_oproj_hg<6>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane);
+    launch_attn_oproj_hg<6>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane,
+                            nt_w);
   else
-    launch_attn_oproj_hg<4>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane);
+    launch_attn_oproj_hg<4>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane,
+                            nt_w);
 }
 
 // Heads per output plane of the fused attention + output projection (K3o), 0 = run
@@ -2145,20 +2167,22 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     const bool cls_only = c.pooling == MQ_POOL_CLS && li + 1 == e->layers.size();
     const int rows = cls_only ? B : M;
     const int stride = cls_only ? L * H : H;
+    const int nt = (int)li >= e->resident_layers ? 1 : 0;  // this layer's weights bypass MALL
     e->tl.mark(s, ST_QKV);
+    RowsArgs qkv{e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1};
+    qkv.nt_w = nt;
     if (li == 0) {  // the embedding gather + LayerNorm run inside the first QKV launch
-      RowsArgs g0{e->word, H, 0, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1};
-      g0.ids = ids;
-      g0.L = L;
-      g0.vocab = c.vocab_size;
-      g0.pos = e->pos;
-      g0.typ = e->typ;
-      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(g0, 0, e->eg, e->eb, eps, e->x.p, s);
+      qkv.A = e->word;
+      qkv.a_plane = 0;
+      qkv.ids = ids;
+      qkv.L = L;
+      qkv.vocab = c.vocab_size;
+      qkv.pos = e->pos;
+      qkv.typ = e->typ;
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(qkv, 0, e->eg, e->eb, eps, e->x.p, s);
     } else {
       const LayerW& p = e->layers[li - 1];
-      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>({e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p,
-                                     3 * H, 0, M, 3 * H, H, 1},
-                                    dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(qkv, dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
     }
     const int qt = cls_only ? 1 : q_tiles;
     int y_planes = 1;
@@ -2168,7 +2192,7 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       y_planes = c.heads / hg;
       const dim3 grid(H / kOpCols, B * qtiles, y_planes);
       ROWS_REP launch_attn_oproj(hg, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wo, w.bo, e->x.p,
-                        stride, e->y.p, (int64_t)rows * H);
+                                 stride, e->y.p, (int64_t)rows * H, nt);
     } else {
       e->tl.mark(s, ST_ATTN);
       if (L <= 64)
@@ -2177,18 +2201,21 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       else
         launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
       e->tl.mark(s, ST_OPROJ);
-      launch_rows<EPI_RESID>({e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1}, s);
+      RowsArgs oproj{e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1};
+      oproj.nt_w = nt;
+      launch_rows<EPI_RESID>(oproj, s);
     }
     e->tl.mark(s, ST_FFN_UP);
-    const RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
+    RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
+    up.nt_w = nt;
     if (c.gelu == MQ_GELU_TANH)
       ROWS_REP launch_rows_ln<EPI_GELU_TANH, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     else
       ROWS_REP launch_rows_ln<EPI_GELU_ERF, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     e->tl.mark(s, ST_FFN_DOWN);
-    ROWS_REP launch_rows<EPI_RESID>({e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F,
-                            dsplit},
-                           s);
+    RowsArgs down{e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F, dsplit};
+    down.nt_w = nt;
+    ROWS_REP launch_rows<EPI_RESID>(down, s);
     prev_rows = rows;
   }
   e->tl.mark(s, ST_POOL);
@@ -2466,6 +2493,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value == 0 || value == 1, "fused_ln must be 0 or 1 (got %d)", value);
       e->fused_ln = value != 0;
       break;
+    case MQ_ENC_OPT_RESIDENT_LAYERS:
+      MQ_CHECK_ARG(value >= 0 && value <= 1024, "resident_layers must be in [0, 1024] (got %d)", value);
+      e->resident_layers = value;
+      break;
     case MQ_ENC_OPT_LN_ON_LOAD:
       MQ_CHECK_ARG(value == 0 || value == 1, "ln_on_load must be 0 or 1 (got %d)", value);
       e->ln_on_load = value != 0;
@@ -2494,6 +2525,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_FUSE_ATTN_OPROJ: *value = e->fuse_attn_oproj ? 1 : 0; break;
     case MQ_ENC_OPT_FUSED_LN: *value = e->fused_ln ? 1 : 0; break;
     case MQ_ENC_OPT_LN_ON_LOAD: *value = e->ln_on_load ? 1 : 0; break;
+    case MQ_ENC_OPT_RESIDENT_LAYERS: *value = e->resident_layers; break;
     case MQ_ENC_OPT_SPLITK_TILES: *value = e->splitk_tiles; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }

@@ -233,7 +233,8 @@ class Encoder:
     OPTIONS = {"rows_max": _lib.MQ_ENC_OPT_ROWS_MAX, "rows_splits": _lib.MQ_ENC_OPT_ROWS_SPLITS,
                "splitk_max": _lib.MQ_ENC_OPT_SPLITK_MAX, "ln_rows_per_wave": _lib.MQ_ENC_OPT_LN_ROWS_PER_WAVE,
                "fuse_attn_oproj": _lib.MQ_ENC_OPT_FUSE_ATTN_OPROJ, "fused_ln": _lib.MQ_ENC_OPT_FUSED_LN,
-               "splitk_tiles": _lib.MQ_ENC_OPT_SPLITK_TILES, "ln_on_load": _lib.MQ_ENC_OPT_LN_ON_LOAD}
+               "splitk_tiles": _lib.MQ_ENC_OPT_SPLITK_TILES, "ln_on_load": _lib.MQ_ENC_OPT_LN_ON_LOAD,
+               "resident_layers": _lib.MQ_ENC_OPT_RESIDENT_LAYERS}
 
     def set_option(self, name, value):
         """Tuning option of the forward (mq_encoder_set_option): rows_max, rows_splits,

@@ -240,6 +240,7 @@ def test_errors(require_gpu):
     ("fused_ln", 1, 70, 32), ("fused_ln", 1, 9, 130),
     ("splitk_tiles", 64, 1, 256), ("splitk_tiles", 4096, 1, 100), ("splitk_tiles", 16, 2, 48),
     ("ln_on_load", 1, 70, 32), ("ln_on_load", 1, 9, 130),
+    ("resident_layers", 0, 1, 32), ("resident_layers", 1, 2, 20), ("resident_layers", 12, 1, 48),
 ])
 def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     """Every non-default value of the explicit tuning options (mq_encoder_set_option,
@@ -262,3 +263,22 @@ def test_options_non_default_values_vs_oracle(require_gpu, name, value, B, L):
     for bad in (-1, 1 << 20):
         with pytest.raises(_lib.MQError):
             enc.set_option(name, bad)
+
+
+def test_resident_layers_changes_only_the_cache_policy(require_gpu):
+    """MQ_ENC_OPT_RESIDENT_LAYERS picks which few-row layers load their weights
+    non-temporally: the forward is bit-identical for every value (fused and two-launch
+    attention paths, the CLS-only last layer)."""
+    cfg = BertConfig(layers=4, max_positions=128)
+    rng = np.random.default_rng(11)
+    enc = Encoder(cfg)
+    for B, L, fuse in ((1, 32, 1), (2, 17, 0)):
+        ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+        mask = np.ones((B, L), np.int32)
+        mask[-1, L // 2:] = 0
+        enc.set_option("fuse_attn_oproj", fuse)
+        outs = []
+        for v in (0, 2, 8):
+            enc.set_option("resident_layers", v)
+            outs.append(enc.embed(ids, mask))
+        assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])

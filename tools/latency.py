@@ -53,6 +53,8 @@ def main():
                     help="comma list of MQ_ENC_OPT_ROWS_MAX values to compare in --encoder-seq-lens mode")
     ap.add_argument("--opt", default="",
                     help="NAME=V1,V2,...: an encoder option (Encoder.OPTIONS) to sweep in --encoder-seq-lens mode")
+    ap.add_argument("--e2e-opt", default="",
+                    help="NAME=V1,V2,...: sweep an encoder option over encoder and end-to-end p50 (L=32, full corpus)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.encoder_seq_lens:
@@ -87,6 +89,17 @@ def main():
     q = torch.empty((1, 768), device=dev)
     s = torch.empty((1, args.k), device=dev)
     i = torch.empty((1, args.k), dtype=torch.int64, device=dev)
+    if args.e2e_opt:
+        name, vals = args.e2e_opt.split("=")
+        res = {}
+        for v in [int(x) for x in vals.split(",")]:
+            enc.set_option(name, v)
+            res["%s=%d" % (name, v)] = {
+                "encoder_ms": p50(lambda: enc.embed_device(ids, mask, q), args.iters),
+                "end_to_end_ms": p50(lambda: (enc.embed_device(ids, mask, q), ix.search_device(q, args.k, s, i)),
+                                     args.iters)}
+        print(res, flush=True)
+        return
     res = {"note": "(p50 ms, min ms) per call; *_stage_ms = device time per kernel class"}
     res["encoder_ms"] = p50(lambda: enc.embed_device(ids, mask, q), args.iters)
     res["search_ms"] = p50(lambda: ix.search_device(q, args.k, s, i), args.iters)
