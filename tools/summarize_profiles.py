@@ -79,11 +79,11 @@ def classify(rows):
     prev = ""
     for did, k, grid, v in rows:
         cls = None
-        if re.search(EXACT_GEMM + r"0>", k):
+        if re.search(EXACT_GEMM + r"0" + LN_ARG, k):
             cls = "qkv_gemm"
-        elif re.search(EXACT_GEMM + r"[12]>", k):
+        elif re.search(EXACT_GEMM + r"[12]" + LN_ARG, k):
             cls = "ffn_up_gemm"
-        elif re.search(EXACT_GEMM + r"3>", k):
+        elif re.search(EXACT_GEMM + r"3" + LN_ARG, k):
             cls = "out_proj_gemm" if "attention" in prev else "ffn_down_gemm" if "gemm_nt_kernel" in prev else None
         else:
             for c, pat in CLASSES.items():
@@ -110,6 +110,8 @@ def mean(v):
 # the exact-f32 encoder GEMM (X6 = false, BF16 = false, optional slice-depth parameter)
 # followed by its epilogue id
 EXACT_GEMM = r"gemm_nt_kernel<mq::F32Tile<\d+, \d+, \d+, \d+, false, \d+, false(, \d+)?>, "
+# ... then gemm_nt_kernel's LN_IN argument (r4: LayerNorm on load, false by default)
+LN_ARG = r"(, (true|false))?>"
 # bench.py kernel class -> kernel-name regex (the encoder GEMM classes are resolved per
 # dispatch by classify())
 CLASSES = {
