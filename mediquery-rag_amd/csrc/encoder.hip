@@ -1647,6 +1647,7 @@ struct GemmArgs {
   float* out;
   int ldo;
   int M, N, K;
+  int nt = 0;  // few-row split-K launches: weights load non-temporally (layers past resident_layers)
 };
 
 template <class T, int EPI, bool LN_IN = false>
@@ -1708,12 +1709,23 @@ int splitk_factor(const GemmArgs& g, int num_cus, int cap = 16, int tiles_max = 
   return best >= 2 ? best : 0;
 }
 
+// The split-K partial GEMM on the 32 x 128 tile (g.nt: non-temporal weight loads).
+void launch_splitk_gemm(const GemmArgs& g, int S, hipStream_t s) {
+  auto go = [&](auto tile) {
+    using T = decltype(tile);
+    const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
+    hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W, g.M, g.N, g.K,
+                       S, g.slab);
+  };
+  if (g.nt)
+    go(F32Tile<1, 4, 1, 1, false, 2, false, 0, true>{});
+  else
+    go(F32Tile<1, 4, 1, 1>{});
+}
+
 template <int EPI>
 void launch_splitk(const GemmArgs& g, int S, hipStream_t s) {
-  using T = F32Tile<1, 4, 1, 1>;
-  const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-  hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W,
-                     g.M, g.N, g.K, S, g.slab);
+  launch_splitk_gemm(g, S, s);
   const int64_t n4 = (int64_t)g.M * g.N / 4;
   hipLaunchKernelGGL((splitk_reduce_kernel<EPI>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
                      s, g.slab, S, g.M, g.N, g.bias, g.resid, g.ldr, g.out, g.ldo);
@@ -1867,11 +1879,8 @@ void gemm_resid_ln(mq_encoder* e, const GemmArgs& g, const float* lng, const flo
     }
   }
   if (S && g.ldr == H && g.N == H) {
-    using T = F32Tile<1, 4, 1, 1>;
     e->tl.mark(s, stage);
-    const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
-    hipLaunchKernelGGL((gemm_splitk_kernel<T>), dim3(tiles * S), dim3(256), 0, s, g.A, g.lda, g.W, g.M,
-                       g.N, g.K, S, g.slab);
+    launch_splitk_gemm(g, S, s);
     e->tl.mark(s, ST_LN);
     hipLaunchKernelGGL((splitk_reduce_ln_kernel<VPL>), dim3((unsigned)g.M), dim3(256), 0, s, g.slab, S,
                        g.M, g.bias, g.resid, g.ldr, lng, lnb, e->cfg.ln_eps, x);
@@ -1940,7 +1949,11 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     // QKV input: x, or (deferred LN2 of the previous layer) y normalised while staged,
     // the column-0 tiles writing LN2(y) to x for the residual and the CLS-row Q GEMM
     const float* qkv_in = y_pending ? e->y.p : e->x.p;
-    auto qkv_gemm = [&](const GemmArgs& g) {
+    // few rows (single queries past the few-row limit): the layers past resident_layers
+    // stream their weights non-temporally in the split-K GEMMs (as forward_rows does)
+    const int lnt = M <= 256 && (int)li >= e->resident_layers ? 1 : 0;
+    auto qkv_gemm = [&](GemmArgs g) {
+      g.nt = lnt;
       if (y_pending) {
         e->tl.mark(s, ST_QKV);
         launch_gemm_ln_in<EPI_BIAS>(g, ln_args(st2, prev->ln2g, prev->ln2b), e->num_cus, s);
@@ -1954,7 +1967,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
       qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0, e->qkv.p + H,
                 3 * H, M, 2 * H, H});
       gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, L * H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, L * 3 * H,
-                         B, H, H},
+                         B, H, H, lnt},
                      ST_QKV, s);
     } else {
       qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H});
@@ -1965,7 +1978,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
     const bool lnl_layer = lnl && !cls_only;
     // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y) - or, deferred, y + partials
-    const GemmArgs oproj{e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H};
+    const GemmArgs oproj{e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H, lnt};
     if (lnl_layer) {
       e->tl.mark(s, ST_OPROJ);
       launch_gemm_stats(oproj, stats_out(st1), e->num_cus, s);
@@ -1973,7 +1986,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
       gemm_resid_ln<VPL>(e, oproj, w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
     }
     const GemmArgs up{e->slab.p, e->slab.n, lnl_layer ? e->y.p : e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F,
-                      rows, F, H};
+                      rows, F, H, lnt};
     if (lnl_layer) {  // FFN-up normalises y (LN1) while staging; its column-0 tiles write x
       e->tl.mark(s, ST_FFN_UP);
       if (c.gelu == MQ_GELU_TANH)
@@ -1985,7 +1998,7 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     } else {
       gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
     }
-    const GemmArgs down{e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F};
+    const GemmArgs down{e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F, lnt};
     if (lnl_layer && li + 1 < e->layers.size()) {  // LN2 deferred into the next layer's QKV
       e->tl.mark(s, ST_FFN_DOWN);
       launch_gemm_stats(down, stats_out(st2), e->num_cus, s);

@@ -35,10 +35,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
 template <int WAVES_M_, int WAVES_N_, int TM_, int TN_, bool X6_ = false, int PF_ = 2,
-          bool BF16_ = false, int BK_ = 0>
+          bool BF16_ = false, int BK_ = 0, bool NTB_ = false>
 struct F32Tile {
   static constexpr int WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TM = TM_, TN = TN_;
   static constexpr bool X6 = X6_;
+  // NTB: B-operand loads are non-temporal (the single-query split-K GEMMs of the layers past
+  // the encoder's resident_layers: their weights stream once and should not evict the
+  // resident layers' weights from MALL)
+  static constexpr bool NTB = NTB_;
   static constexpr int PF = PF_;  // register prefetch depth in slices (walk_tiles D)
   // BF16: both operands are bf16 in memory, addressed as float-typed rows of half the
   // width (two bf16 per 4-byte slot): the staging is byte-identical to the f32 path and
@@ -141,7 +145,7 @@ struct Stager {
                                                  ra, min(row, alim) * a4 + ch * 16, k0 * 4, 0));
         else
           r[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 rb, min(row - T::BM, blim) * b4 + ch * 16, k0 * 4, 0));
+                                                 rb, min(row - T::BM, blim) * b4 + ch * 16, k0 * 4, T::NTB ? 2 : 0));
       }
       return;
     }
