@@ -1628,8 +1628,8 @@ void launch_fallback_scans(mq_index* ix, int64_t nq, int k, const int* nf, const
 // block from screen_verify_kernel; k <= 16), results written into os / oi; nothing is
 // read back.  fallback_prepare sizes the workspace (before the verify launch, which
 // writes the compact block) and says whether the asynchronous path applies: not when the
-// worst-case candidate lists would take more than kFbMaxBytes (very large batches stay
-// synchronous).
+// worst-case candidate lists plus the compact query block would take more than kFbMaxBytes
+// (very large batches stay synchronous).
 constexpr size_t kFbMaxBytes = 256ull << 20;
 
 struct FallbackPlan {
@@ -1643,7 +1643,10 @@ int fallback_prepare(mq_index* ix, int64_t nq, int k, FallbackPlan* fp) {
   fallback_extent<SearchNarrow>(ix, 1, std::min<int64_t>(nq, kFbNarrowMax), per_cu, k, &grid_n, &cand);
   if (nq > kFbNarrowMax) fallback_extent<SearchWide>(ix, kFbNarrowMax + 1, nq, per_cu, k, &grid_w, &cand);
   fp->ok = false;
-  if ((size_t)cand * (sizeof(float) + sizeof(int)) > kFbMaxBytes) return MQ_OK;
+  // the budget counts the compact query block too (nq x dim floats): a batch of
+  // millions of queries with small k stays synchronous instead of keeping a second copy
+  if ((size_t)cand * (sizeof(float) + sizeof(int)) + (size_t)nq * ix->dim * sizeof(float) > kFbMaxBytes)
+    return MQ_OK;
   int rc = ix->afb_q.ensure((size_t)nq * ix->dim * sizeof(float));
   if (!rc) rc = ix->afb_cs.ensure((size_t)cand * sizeof(float));
   if (!rc) rc = ix->afb_ci.ensure((size_t)cand * sizeof(int));
@@ -1662,6 +1665,8 @@ int fallback_prepare(mq_index* ix, int64_t nq, int k, FallbackPlan* fp) {
   return MQ_OK;
 }
 
+// launch_fallback_scans' list widths are 8 / 16: the async path runs only for k <= kScreenMaxK
+static_assert(kScreenMaxK <= 16, "fallback_search_kernel<KC> has KC = 8 or 16");
 int launch_async_fallback(mq_index* ix, const FallbackPlan& fp, int64_t nq, int k, float* os, int64_t* oi,
                           const int64_t* fail, hipStream_t s) {
   const int* nf = ix->flag.as<int>();
@@ -1723,7 +1728,7 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     FallbackPlan fp;
     if (tier == TIER_BF16) {
       poll_async_fallbacks(ix);
-      if (ix->async_screen && ix->sync_left == 0 && k <= 16) {
+      if (ix->async_screen && ix->sync_left == 0 && k <= kScreenMaxK) {
         rc = fallback_prepare(ix, nq, k, &fp);
         if (rc) return rc;
       }
@@ -2128,20 +2133,31 @@ int mq_index_screen_fallbacks(const mq_index* cix, int64_t* to_direct, int64_t* 
   clear_error();
   MQ_CHECK_ARG(cix, "NULL argument");
   mq_index* ix = const_cast<mq_index*>(cix);  // the counters are folded in under the lock
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (ix->afb_event) {
-    DeviceGuard dg(ix->device);
-    MQ_HIP(hipEventSynchronize(ix->afb_event));
-    poll_async_fallbacks(ix);
+  // The wait runs WITHOUT the lock: a counter read must not block searches on
+  // other threads until the last asynchronous batch lands.  Take the event under the lock,
+  // wait, then re-lock to fold the count in; a search recorded meanwhile re-records the
+  // event, so the count is exact as of the wait (eventually consistent after it).
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ix->mu);
+    ev = ix->afb_event;
   }
+  if (ev) {
+    DeviceGuard dg(ix->device);
+    MQ_HIP(hipEventSynchronize(ev));
+  }
+  std::lock_guard<std::mutex> lk(ix->mu);
+  poll_async_fallbacks(ix);
   if (to_direct) *to_direct = ix->screen_fallbacks;
   if (to_split) *to_split = ix->screen_passdowns;
   return MQ_OK;
 }
 
-int mq_index_screen_skips(const mq_index* ix, int64_t* bf16_skips, int64_t* int8_skips) {
+int mq_index_screen_skips(const mq_index* cix, int64_t* bf16_skips, int64_t* int8_skips) {
   clear_error();
-  MQ_CHECK_ARG(ix, "NULL argument");
+  MQ_CHECK_ARG(cix, "NULL argument");
+  mq_index* ix = const_cast<mq_index*>(cix);  // read under the lock, as its sibling getters
+  std::lock_guard<std::mutex> lk(ix->mu);
   if (bf16_skips) *bf16_skips = ix->bf_skips;
   if (int8_skips) *int8_skips = ix->i8_skips;
   return MQ_OK;

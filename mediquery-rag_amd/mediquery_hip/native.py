@@ -238,7 +238,10 @@ class Encoder:
 
     def set_option(self, name, value):
         """Tuning option of the forward (mq_encoder_set_option): rows_max, rows_splits,
-        splitk_max, ln_rows_per_wave, fuse_attn_oproj, fused_ln, splitk_tiles, ln_on_load."""
+        splitk_max, ln_rows_per_wave, fuse_attn_oproj, fused_ln, splitk_tiles, ln_on_load,
+        resident_layers (0..1024, default 8: the few-row forward loads layers below this
+        index with the default cache policy and later layers non-temporally, so the first
+        layers' weights stay in MALL between single queries; outputs are bit-identical)."""
         _lib.call("mq_encoder_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name):
