@@ -236,6 +236,10 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *                                in MALL (0..1024, default 8: BERT-base single query
  *                                0.446 -> 0.427 ms encoder p50; 0 = all non-temporal is the
  *                                slowest, 0.463)
+ *   MQ_ENC_OPT_X6_PRESPLIT       split-f32 precision, batched GEMMs: 1 (default) = K2p on the
+ *                                weights' W3 plane images (split once, at weight load or
+ *                                set_precision), 0 = the split-f32 tiles that split both
+ *                                operands while staging them.  Bit-identical results.
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
@@ -246,6 +250,7 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 #define MQ_ENC_OPT_SPLITK_TILES 6
 #define MQ_ENC_OPT_LN_ON_LOAD 7
 #define MQ_ENC_OPT_RESIDENT_LAYERS 8
+#define MQ_ENC_OPT_X6_PRESPLIT 9
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);
@@ -283,6 +288,18 @@ int mq_tokenizer_encode_batch(mq_tokenizer* tok, const char* const* texts, int n
  * 128x64, 8 / 9 = exact / split-f32 128x192 on 8-wave workgroups.  K % 32 == 0.  For
  * kernel unit tests. */
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
+                      float* out, int M, int N, int K, int epi, int tile, void* stream);
+/* The W3 plane image of a weight W [N][K] (K % 16 == 0): three bf16 planes of
+ * the exact split in 1 KB MFMA fragments.  mq_debug_w3_bytes gives its size (-1 for a bad
+ * shape), mq_debug_split_w3 writes it (device buffers, asynchronous on `stream`). */
+int64_t mq_debug_w3_bytes(int N, int K);
+int mq_debug_split_w3(const float* W, int N, int K, void* w3, void* stream);
+/* The encoder GEMM on the pre-split split-f32 kernel (K2p) with W given as its W3 image:
+ * tile 0 = 128x192, 1 = 256x96 (4 compute + 4 loader waves), 2 = 128x192, 3 = 256x192
+ * (8 compute waves), -1 = the default pick; 4-7 = measurement variants (gemm_x6p.hip).
+ * Bit-identical to the split-f32 tiles 5-7 / 9 of mq_debug_gemm_f32.  Asynchronous on
+ * `stream`.  K % 32 == 0. */
+int mq_debug_gemm_x6p(const float* A, const void* W3, const float* bias, const float* resid,
                       float* out, int M, int N, int K, int epi, int tile, void* stream);
 
 /* The int8 screen (K9q) alone for one host query: its kc candidates (screen scores

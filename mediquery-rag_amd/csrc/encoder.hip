@@ -23,13 +23,12 @@
 #include <vector>
 
 #include "common.hpp"
+#include "gemm_epi.hpp"
 #include "gemm_f32.hpp"
+#include "gemm_x6p.hpp"
 
 namespace mq {
 
-// EPI_RESID_STATS: EPI_RESID that also leaves per-row LayerNorm partials of its output
-// (the LayerNorm is then applied by the consuming GEMM while it stages A: LnArgs below).
-enum Epi { EPI_BIAS = 0, EPI_GELU_ERF = 1, EPI_GELU_TANH = 2, EPI_RESID = 3, EPI_RESID_STATS = 4 };
 
 // LayerNorm deferred into the consumer (batched path, MQ_ENC_OPT_LN_ON_LOAD).  The
 // residual GEMM (out-proj / FFN-down, EPI_RESID_STATS) writes y = A W^T + b + resid and,
@@ -52,36 +51,6 @@ struct LnArgs {
   int nt;                 // partials per row (K / kLnPartW)
   float eps;
 };
-
-// GELU, branch-free (it runs 64 times per lane in every FFN-up tile epilogue; ocml's erff
-// is ~50 VALU + a divergent branch per element and measured as the FFN-up epilogue's cost).
-// erf form: x * Phi(x), Phi(x) = 0.5 erfc(-x / sqrt 2), with erfc(z) for z = |x| / sqrt 2 from
-// the Chebyshev fit t * exp(-z^2 + P(t)), t = 1 / (1 + z / 2) (Numerical Recipes erfcc,
-// |relative error| < 1.2e-7 for all z >= 0): Phi = 1 - e / 2 for x >= 0, e / 2 below.  No
-// 1 + erf cancellation for negative x: max |error| vs float64 3.8e-7 over [-12, 12], relative
-// 1.7e-6 where |gelu| > 1e-3 (0.5 x (1 + erff) in fp32: 4.5e-7 and 5.1e-5).  v_rcp / v_exp
-// are the hardware 1-ulp forms.
-__device__ __forceinline__ float gelu_erf(float x) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float e = t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.4426950408889634f);  // erfc(z)
-  return x * (x >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e);
-}
-// tanh form (llama.cpp's): 0.5 x (1 + tanh u) = x / (1 + exp(-2u)), u = sqrt(2/pi)(x + 0.044715 x^3)
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.7978845608028654f * fmaf(0.044715f * x, x * x, x);
-  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -2.8853900817779268f));
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -1622,6 +1591,9 @@ struct Buf {
 
 struct LayerW {
   const float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
+  // W3 plane images of the four projection weights (gemm_x6p.hpp), built when the split-f32
+  // precision is selected; null otherwise
+  const unsigned char *wqkv3 = nullptr, *wo3 = nullptr, *w13 = nullptr, *w23 = nullptr;
 };
 
 int64_t weight_count(const mq_bert_config& c) {
@@ -1648,6 +1620,7 @@ struct GemmArgs {
   int ldo;
   int M, N, K;
   int nt = 0;  // few-row split-K launches: weights load non-temporally (layers past resident_layers)
+  const void* W3 = nullptr;  // split-f32: W's W3 plane image (K2p, gemm_x6p.hip)
 };
 
 template <class T, int EPI, bool LN_IN = false>
@@ -1739,7 +1712,12 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false,
     launch_splitk<EPI>(g, S, s);
     return;
   }
-  if (x6) {  // split-f32 tiles: same waste model over 128x{128,96,64}
+  if (x6 && g.W3) {  // split-f32 on the pre-split weights (K2p)
+    launch_gemm_x6p(X6pArgs{g.A, g.lda, g.W3, g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K}, EPI, -1, num_cus,
+                    s);
+    return;
+  }
+  if (x6) {  // split-f32 tiles (both operands split while staged): same waste model over 128x{128,96,64}
     const int bns[3] = {128, 96, 64};
     const double effs[3] = {1.0, 0.96, 0.9};
     const int64_t slots = 2 * (int64_t)num_cus;
@@ -1811,6 +1789,7 @@ struct mq_encoder {
   const float *word = nullptr, *pos = nullptr, *typ = nullptr, *eg = nullptr, *eb = nullptr;
   std::vector<LayerW> layers;
   Buf x, y, qkv, ctx, ffn, io_out, slab;  // (+ lnst below)
+  Buf w3;  // split-f32: every layer's W3 plane images (LayerW::*3 point into it)
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -1840,6 +1819,7 @@ struct mq_encoder {
   bool ln_on_load = false;      // batched forward: LayerNorm applied by the consuming GEMM (LnArgs;
                                 // measured slower: the consumers' staging VALU)
   Buf lnst;                     // its per-row partials, two sets of [M][H / kLnPartW] (mean, M2)
+  bool x6_presplit = true;      // split-f32 batched GEMMs on the W3 images (K2p)
   bool use_graphs = false;  // eager measured faster for one query (0.628 vs 0.645 ms: the
                             // graph path stages ids / mask / out through its own buffers)
   uint64_t graph_clock = 0;
@@ -1849,10 +1829,41 @@ struct mq_encoder {
 
 namespace {
 
+// Split-f32 precision: split every layer's four projection weights once into their W3
+// plane images (gemm_x6p.hpp; 6 B per weight, 510 MB for BERT-base), which the batched
+// GEMMs (K2p) multiply without re-splitting them.  No-op unless the precision is F32X6 and
+// weights are loaded, or when the images exist.  Synchronous.
+int build_w3(mq_encoder* e) {
+  if (e->precision != MQ_DTYPE_F32X6 || !e->loaded || e->layers.empty() || e->layers[0].wqkv3) return MQ_OK;
+  const mq_bert_config& c = e->cfg;
+  const int H = c.hidden, F = c.ffn;
+  const size_t per = w3_bytes(3 * H, H) + w3_bytes(H, H) + w3_bytes(F, H) + w3_bytes(H, F);
+  DeviceGuard dg(e->device);
+  int rc = e->w3.ensure((per * e->layers.size() + 3) / 4);
+  if (rc) return rc;
+  unsigned char* p = reinterpret_cast<unsigned char*>(e->w3.p);
+  for (LayerW& w : e->layers) {
+    auto one = [&](const float* W, int n, int k, const unsigned char*& dst) {
+      launch_split_w3(W, n, k, p, nullptr);
+      dst = p;
+      p += w3_bytes(n, k);
+    };
+    one(w.wqkv, 3 * H, H, w.wqkv3);
+    one(w.wo, H, H, w.wo3);
+    one(w.w1, F, H, w.w13);
+    one(w.w2, H, F, w.w23);
+  }
+  MQ_HIP(hipGetLastError());
+  MQ_HIP(hipStreamSynchronize(nullptr));
+  return MQ_OK;
+}
+
 template <int EPI>
 void gemm(mq_encoder* e, const GemmArgs& g, int stage, hipStream_t s) {
   e->tl.mark(s, stage);
-  launch_gemm<EPI>(g, e->num_cus, s, e->precision == MQ_DTYPE_F32X6, e->splitk_max, e->splitk_tiles);
+  GemmArgs a = g;
+  if (!e->x6_presplit) a.W3 = nullptr;
+  launch_gemm<EPI>(a, e->num_cus, s, e->precision == MQ_DTYPE_F32X6, e->splitk_max, e->splitk_tiles);
 }
 
 // Residual projection + LayerNorm: x = LN(A W^T + b + resid), through y (g.out) on the
@@ -1964,13 +1975,17 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     if (cls_only && L > 1) {
       // only the CLS rows need queries: K and V for every token ([M, 2H] into qkv columns
       // H..3H), Q for the B CLS rows (every L-th row of x into row b*L of qkv)
-      qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0, e->qkv.p + H,
-                3 * H, M, 2 * H, H});
-      gemm<EPI_BIAS>(e, {e->slab.p, e->slab.n, e->x.p, L * H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, L * 3 * H,
-                         B, H, H, lnt},
-                     ST_QKV, s);
+      GemmArgs kv{e->slab.p, e->slab.n, qkv_in, H, w.wqkv + (int64_t)H * H, w.bqkv + H, nullptr, 0, e->qkv.p + H,
+                  3 * H, M, 2 * H, H};
+      if (w.wqkv3) kv.W3 = w.wqkv3 + w3_row_offset(H, H);
+      qkv_gemm(kv);
+      GemmArgs q{e->slab.p, e->slab.n, e->x.p, L * H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, L * 3 * H, B, H, H, lnt};
+      q.W3 = w.wqkv3;
+      gemm<EPI_BIAS>(e, q, ST_QKV, s);
     } else {
-      qkv_gemm({e->slab.p, e->slab.n, qkv_in, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H});
+      GemmArgs qkv{e->slab.p, e->slab.n, qkv_in, H, w.wqkv, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, M, 3 * H, H};
+      qkv.W3 = w.wqkv3;
+      qkv_gemm(qkv);
     }
     y_pending = false;
     e->tl.mark(s, ST_ATTN);
@@ -1978,15 +1993,17 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
     const bool lnl_layer = lnl && !cls_only;
     // x = LN1(x + ctx Wo^T + bo)  (compact [rows, H], through y) - or, deferred, y + partials
-    const GemmArgs oproj{e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H, lnt};
+    GemmArgs oproj{e->slab.p, e->slab.n, e->ctx.p, stride, w.wo, w.bo, e->x.p, stride, e->y.p, H, rows, H, H, lnt};
+    oproj.W3 = w.wo3;
     if (lnl_layer) {
       e->tl.mark(s, ST_OPROJ);
       launch_gemm_stats(oproj, stats_out(st1), e->num_cus, s);
     } else {
       gemm_resid_ln<VPL>(e, oproj, w.ln1g, w.ln1b, e->x.p, ST_OPROJ, s);
     }
-    const GemmArgs up{e->slab.p, e->slab.n, lnl_layer ? e->y.p : e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F,
-                      rows, F, H, lnt};
+    GemmArgs up{e->slab.p, e->slab.n, lnl_layer ? e->y.p : e->x.p, H, w.w1, w.b1, nullptr, 0, e->ffn.p, F,
+                rows, F, H, lnt};
+    up.W3 = w.w13;
     if (lnl_layer) {  // FFN-up normalises y (LN1) while staging; its column-0 tiles write x
       e->tl.mark(s, ST_FFN_UP);
       if (c.gelu == MQ_GELU_TANH)
@@ -1998,7 +2015,8 @@ int forward_vpl(mq_encoder* e, const int* ids, const int* mask, int B, int L, fl
     } else {
       gemm<EPI_GELU_ERF>(e, up, ST_FFN_UP, s);
     }
-    const GemmArgs down{e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F, lnt};
+    GemmArgs down{e->slab.p, e->slab.n, e->ffn.p, F, w.w2, w.b2, e->x.p, H, e->y.p, H, rows, H, F, lnt};
+    down.W3 = w.w23;
     if (lnl_layer && li + 1 < e->layers.size()) {  // LN2 deferred into the next layer's QKV
       e->tl.mark(s, ST_FFN_DOWN);
       launch_gemm_stats(down, stats_out(st2), e->num_cus, s);
@@ -2413,7 +2431,7 @@ int mq_encoder_load_weights(mq_encoder* e, const float* blob, int64_t n_floats) 
     e->layers.push_back(w);
   }
   e->loaded = true;
-  return MQ_OK;
+  return build_w3(e);  // (re)split the new weights when the split-f32 precision is selected
 }
 
 int mq_encoder_set_precision(mq_encoder* e, int dtype) {
@@ -2423,7 +2441,7 @@ int mq_encoder_set_precision(mq_encoder* e, int dtype) {
                "encoder precision must be MQ_DTYPE_F32 or MQ_DTYPE_F32X6 (got %d)", dtype);
   std::lock_guard<std::mutex> lk(e->mu);
   e->precision = dtype;
-  return MQ_OK;
+  return build_w3(e);
 }
 
 int mq_debug_gemm_f32(const float* A, const float* W, const float* bias, const float* resid,
@@ -2518,6 +2536,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value >= 0 && value <= 4096, "splitk_tiles must be in [0, 4096] (got %d)", value);
       e->splitk_tiles = value;
       break;
+    case MQ_ENC_OPT_X6_PRESPLIT:
+      MQ_CHECK_ARG(value == 0 || value == 1, "x6_presplit must be 0 or 1 (got %d)", value);
+      e->x6_presplit = value != 0;
+      break;
     default:
       MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
@@ -2540,6 +2562,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_LN_ON_LOAD: *value = e->ln_on_load ? 1 : 0; break;
     case MQ_ENC_OPT_RESIDENT_LAYERS: *value = e->resident_layers; break;
     case MQ_ENC_OPT_SPLITK_TILES: *value = e->splitk_tiles; break;
+    case MQ_ENC_OPT_X6_PRESPLIT: *value = e->x6_presplit ? 1 : 0; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
   return MQ_OK;

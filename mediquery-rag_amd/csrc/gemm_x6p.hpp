@@ -1,0 +1,54 @@
+// gemm_x6p.hpp - host interface of the pre-split split-f32 GEMM (gemm_x6p.hip).
+//
+// The split-f32 ("x6") arithmetic of gemm_f32.hpp - every fp32 operand split exactly into
+// three bf16 planes, six v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation - with
+// the weight operand split ONCE, when the weights are loaded, into a fragment-blocked
+// plane image ("W3"):
+//
+//   W3[nb][kb][p][h][r][j]  bf16,  row n = 32 nb + r, k = 16 kb + 8 h + j, plane p = 0..2
+//
+// i.e. per 32-row x 16-k block and plane one 1 KB MFMA operand fragment in lane order
+// (lane = 32 h + r holds 16 B): one LDS-DMA wave-instruction moves it HBM -> LDS whole and
+// one conflict-free ds_read_b128 hands it to the MFMA.  Rows past N are zero (N is padded
+// to a multiple of 32).  The activation operand stays fp32 in HBM; it is staged fp32 and
+// split while its fragments are read.  Products and their order are those of the
+// split-f32 tiles of gemm_f32.hpp: results are bit-identical to them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace mq {
+
+// bytes of the W3 image of an N x K weight (K % 16 == 0)
+inline size_t w3_bytes(int64_t N, int64_t K) { return (size_t)((N + 31) / 32) * (size_t)(K / 16) * 3 * 1024; }
+// byte offset of row block `row0` (a multiple of 32) inside a W3 image of depth K: the
+// image of rows [row0, N) of W is the tail of W's image
+inline size_t w3_row_offset(int64_t row0, int64_t K) { return (size_t)(row0 / 32) * (size_t)(K / 16) * 3 * 1024; }
+
+// split W [N][K] fp32 (row stride K) into its W3 image (w3_bytes(N, K) bytes)
+void launch_split_w3(const float* W, int N, int K, void* w3, hipStream_t s);
+
+struct X6pArgs {
+  const float* A;  // [M][lda] fp32 activations
+  int lda;
+  const void* W3;  // W3 image of W [N][K]
+  const float* bias;
+  const float* resid;
+  int ldr;
+  float* out;
+  int ldo;
+  int M, N, K;  // K % 16 == 0
+};
+
+// Tile shapes (workgroups of 8 waves, one per CU): 0 = 128 x 192 (4 compute + 4 loader
+// waves; the default: M = 8192 at N = 768 / 1536 / 2304 / 3072 gives whole rounds of 256
+// tiles), 1 = 256 x 96 (same waves), 2 = 128 x 192 and 3 = 256 x 192 (8 compute waves).
+// -1 = the pick below.
+int x6p_pick_tile(int M, int N, int num_cus);
+// epi: EPI_BIAS / EPI_GELU_ERF / EPI_GELU_TANH / EPI_RESID (gemm_epi.hpp)
+void launch_gemm_x6p(const X6pArgs& g, int epi, int tile, int num_cus, hipStream_t s);
+
+}  // namespace mq

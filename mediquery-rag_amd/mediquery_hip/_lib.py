@@ -24,6 +24,7 @@ MQ_MAX_K = 64
 MQ_ENC_OPT_ROWS_MAX, MQ_ENC_OPT_ROWS_SPLITS, MQ_ENC_OPT_SPLITK_MAX = 0, 1, 2
 MQ_ENC_OPT_LN_ROWS_PER_WAVE, MQ_ENC_OPT_FUSE_ATTN_OPROJ, MQ_ENC_OPT_FUSED_LN = 3, 4, 5
 MQ_ENC_OPT_SPLITK_TILES, MQ_ENC_OPT_LN_ON_LOAD, MQ_ENC_OPT_RESIDENT_LAYERS = 6, 7, 8
+MQ_ENC_OPT_X6_PRESPLIT = 9
 
 
 class MQError(RuntimeError):
@@ -98,6 +99,9 @@ SIGNATURES = {
     "mq_tokenizer_encode_batch": (_I, [_P, ctypes.POINTER(ctypes.c_char_p), _I, _I, _P, _P,
                                        ctypes.POINTER(_I)]),
     "mq_debug_gemm_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "mq_debug_w3_bytes": (_I64, [_I, _I]),
+    "mq_debug_split_w3": (_I, [_P, _I, _I, _P, _P]),
+    "mq_debug_gemm_x6p": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "mq_debug_int8_screen": (_I, [_P, _P, _I, _P, _P, _P]),
 }
 

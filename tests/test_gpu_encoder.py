@@ -282,3 +282,33 @@ def test_resident_layers_changes_only_the_cache_policy(require_gpu):
             enc.set_option("resident_layers", v)
             outs.append(enc.embed(ids, mask))
         assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("B,L,layers,pool", [
+    (256, 32, 12, None),           # the bench shape: every batched GEMM on K2p
+    (9, 33, 3, POOL_MEAN),         # 297 rows: ragged 128-row tiles
+    (9, 33, 3, None),              # CLS-only last layer: K/V rows of the W3 image
+    (300, 3, 2, None),             # many short sequences
+])
+def test_x6_presplit_bit_identical(require_gpu, B, L, layers, pool):
+    """Split-f32 precision: the batched GEMMs on the pre-split W3 weights (K2p, default)
+    give the same bits as the split-f32 tiles that re-split both operands (x6_presplit =
+    0) - same planes, same six products in the same order - and match the oracle."""
+    kw = {"layers": layers}
+    if pool is not None:
+        kw["pooling"] = pool
+    cfg = BertConfig(**kw) if layers != 12 else DMETA_BASE
+    rng = np.random.default_rng(B * 5 + L)
+    ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    for b in range(0, B, 3):
+        mask[b, int(rng.integers(1, L + 1)):] = 0
+    enc = Encoder(cfg)
+    enc.set_precision(_lib.MQ_DTYPE_F32X6)
+    assert enc.get_option("x6_presplit") == 1
+    got = enc.embed(ids, mask)
+    enc.set_option("x6_presplit", 0)
+    old = enc.embed(ids, mask)
+    assert np.array_equal(got, old), float(np.abs(got - old).max())
+    ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
+    _close(got, ref)
