@@ -2291,7 +2291,7 @@ constexpr size_t kMaxGraphs = 6;
 int launch_graph(mq_encoder* e, int B, int L, hipStream_t s) {
   const std::vector<const void*> bufs = {e->weights.p, e->x.p,   e->y.p,      e->qkv.p,
                                          e->ctx.p,     e->ffn.p, e->slab.p,   e->io_out.p,
-                                         e->io_ids,    e->io_mask};
+                                         e->io_ids,    e->io_mask,  e->w3.p};
   mq_encoder::Graph* hit = nullptr;
   for (auto& g : e->graphs)
     if (g.B == B && g.L == L && g.precision == e->precision && g.bufs == bufs) hit = &g;

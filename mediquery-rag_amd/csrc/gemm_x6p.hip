@@ -505,8 +505,8 @@ using X6p1 = X6pTile<4, 1, 2, 3, 4, 1, 4, true, 0, 1, 0, 6, true>;  // 256 x 96,
 using X6p2 = X6pTile<4, 2, 1, 3, 4, 1, 4, true, 0, 2, 1, 6>;        // 128 x 192, 8 waves, DMAs from 0-3
 using X6p3 = X6pTile<4, 2, 2, 3, 4, 1, 8, true, 0, 6, 1, 8>;        // 256 x 192, 8 waves
 // measurement variants (tile codes 4-7)
-using X6p4 = X6pTile<4, 2, 1, 3, 4>;                                // 128 x 192, first cut
-using X6p5 = X6pTile<4, 2, 2, 3, 4>;                                // 256 x 192, first cut
+using X6p4 = X6pTile<2, 2, 2, 3, 3, 2, 4, true, 0, 1, 0, 6, true>;  // tile 0 with 32-deep stages, 3 slots
+using X6p5 = X6pTile<2, 2, 2, 3, 4, 1, 4, true, 0, 1, 0, 4, true>;  // tile 0, split from slot 4
 using X6p6 = X6pTile<2, 2, 2, 3, 5, 1, 4, true, 0, 1, 0, 6, true>;  // tile 0 with 5 slots
 using X6p7 = X6pTile<2, 2, 2, 3, 4, 1, 4, true, 0, 1, 0, 10, true>; // tile 0, split from slot 10
 
@@ -527,14 +527,14 @@ void launch_tile(const X6pArgs& g, int tile, int num_cus, hipStream_t s) {
 #ifdef MQ_X6P_DBG
   if (tile >= 8) {  // measurement builds: tiles 1 / 0 minus parts (X6pTile DBG bits)
     switch (tile) {
-      case 8: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 64>, EPI>(g, num_cus, s); return;
-      case 9: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 8>, EPI>(g, num_cus, s); return;
-      case 10: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 256>, EPI>(g, num_cus, s); return;
-      case 11: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 512>, EPI>(g, num_cus, s); return;
-      case 12: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 72>, EPI>(g, num_cus, s); return;
-      case 13: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 74>, EPI>(g, num_cus, s); return;
-      case 14: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 200>, EPI>(g, num_cus, s); return;
-      default: launch_t<X6pTile<4, 2, 1, 3, 4, 1, 8, true, 202>, EPI>(g, num_cus, s); return;
+      case 8: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 64, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 9: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 66, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 10: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 8, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 11: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 74, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 12: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 2, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 13: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 256, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      case 14: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 512, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
+      default: launch_t<X6pTile<2, 2, 2, 3, 4, 1, 4, true, 128, 1, 0, 6, true>, EPI>(g, num_cus, s); return;
     }
   }
 #endif

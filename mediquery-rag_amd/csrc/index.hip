@@ -539,116 +539,232 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
   }
 }
 
-#ifndef MQ_FIN_DBG  // measurement builds only (wrong results): 1 = no survivor ranking, 2 = no re-rank gathers
+#ifndef MQ_FIN_DBG  // measurement builds only (wrong results): 1 = no survivor ranking, 2 = no re-rank gathers,
+                    // 4 = return at once, 8 = no survivors loaded, 16 = phase times (printf, 100 MHz ticks)
 #define MQ_FIN_DBG 0
 #endif
 #if MQ_FIN_DBG != 0 && !defined(MQ_MEASUREMENT_BUILD)
 #error "MQ_FIN_DBG computes wrong results: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
 #endif
-constexpr int kFinW = 8, kFinT = 64 * kFinW;  // K9q finish: 8 waves, all 64 re-rank gathers in one round
+// rank of (x, xi) by (score desc, id asc) among n4 * 4 LDS entries (vs, vi): float4 /
+// int4 reads, unrolled so the reads pipeline (an early-exit scalar loop paid the LDS
+// latency per entry: ~38 us for 320 survivors)
+__device__ __forceinline__ int lds_rank4(const floatx4* vs, const int4* vi, int n4, float x, int xi) {
+  int r = 0;
+#pragma unroll 4
+  for (int j = 0; j < n4; ++j) {
+    const floatx4 a = vs[j];
+    const int4 b = vi[j];
+    r += (a.x > x || (a.x == x && b.x < xi)) + (a.y > x || (a.y == x && b.y < xi)) +
+         (a.z > x || (a.z == x && b.z < xi)) + (a.w > x || (a.w == x && b.w < xi));
+  }
+  return r;
+}
+
+// order-preserving float <-> unsigned (key 0 is below every float)
+__device__ __forceinline__ unsigned fin_ord(float x) {
+  const unsigned b = __float_as_uint(x);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fin_unord(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+constexpr int kScreenMaxK = 16;  // screened (certified) searches: k <= 16
+constexpr int kFinW = 8, kFinT = 64 * kFinW;  // K9q finish: 8 waves, 64 re-rank gathers per round
+constexpr int kFinMaxSurv = 1024;  // survivors the finish ranks (more: the query is passed down)
+constexpr int kFinLive = 512;      // live candidates it re-ranks (more: passed down)
 // K9q finish, one block per query (the single-query int8 screen, fused to save launches
-// on the latency path): the survivors' top-kc by screen score (as bf16_select_kernel:
-// slots past the survivors hold (tau, -1), more than kTsCap survivors -> bound +inf),
-// the exact fp32 re-rank of the prefix that can still reach the top-k (screen >=
-// s_k - 2E, as rerank_kernel), the top-k by (score desc, id asc), and the certificate
-// s_kc + E < e_k (as screen_verify_kernel, mode VERIFY_BF16_Q32 with the int8 maxima).
+// on the latency path).  The threshold scan kept every row whose screen score s clears
+// tau (count[q] of them, at most kTsCap stored).  The screen's error on row r is bounded
+// by E_r (the VERIFY_BF16_Q32 form of screen_bound with the row's own int8 error
+// ||c_r - scale_r r8_r|| in place of the shadow's maximum; E >= every E_r is the global
+// form):
+//  * lo_r = s_r - E_r <= exact_r <= s_r + E_r = hi_r; with L_k the k-th largest lo among
+//    the survivors, k survivors have exact >= L_k, so a survivor with hi_r < L_k cannot
+//    reach the exact top-k: only the live survivors hi_r >= L_k are re-ranked in fp32 (as
+//    rerank_kernel: same dot arithmetic), and their top-k by (score desc, id asc) is the
+//    answer among the survivors (the per-row bound keeps ~half the live rows of the r5
+//    global s >= cs_k - 2E rule on isotropic data: fewer gather rounds);
+//  * a row that did not survive has s < tau, exact < tau + E: the answer is certified
+//    when tau + E < e_k (the k-th exact score), with every survivor kept and ranked and
+//    every live one re-ranked.
+// The certificate is against tau itself, not the 64th-best survivor (r4): on a clustered
+// corpus the query's cluster-mates crowd the top 64 screen scores within the int8 bound,
+// while tau - set by the scan from the sample pass (i8_thresh_kernel: at most the k-th
+// best sample - 2E) - sits below e_k - E.
 __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restrict__ Q,
                                                         const float* __restrict__ rows, int dim,
                                                         const float* __restrict__ ts_cs,
                                                         const int* __restrict__ ts_ci,
                                                         const int* __restrict__ count,
-                                                        const float* __restrict__ tau, int kc, int k,
+                                                        const float* __restrict__ tau, int k,
                                                         const unsigned* __restrict__ stats,
+                                                        const float* __restrict__ err8,
                                                         float* __restrict__ os, int64_t* __restrict__ oi,
                                                         int* __restrict__ n_fail,
                                                         int64_t* __restrict__ fail) {
-  __shared__ float ls[kTsCap];
-  __shared__ int li[kTsCap];
-  __shared__ float cs[MQ_MAX_K], sc[MQ_MAX_K];
-  __shared__ int ci[MQ_MAX_K];
-  __shared__ long long sid[MQ_MAX_K];
-  __shared__ float e_sh, ek_sh;
-  __shared__ int live_sh;
+  // lo / li and sc / sid are padded to a multiple of 4 with (-inf, INT_MAX), never better
+  // than a real entry: the rank counts read them as float4 / int4 (lds_rank4)
+  __shared__ float ls[kFinMaxSurv];  // hi_r
+  __shared__ floatx4 lo4[kFinMaxSurv / 4];
+  __shared__ int4 li4[kFinMaxSurv / 4];
+  __shared__ floatx4 sc4[kFinLive / 4];
+  __shared__ int4 sid4[kFinLive / 4];
+  __shared__ int lv[kFinLive];
+  __shared__ unsigned long long wk[kFinW * kScreenMaxK];
+  float* lo = reinterpret_cast<float*>(lo4);
+  int* li = reinterpret_cast<int*>(li4);
+  float* sc = reinterpret_cast<float*>(sc4);
+  int* sid = reinterpret_cast<int*>(sid4);
+  __shared__ float e_sh, qn_sh, ek_sh, lk_sh;
+  __shared__ int nlive_sh;
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int total = count[q];
-  const int cnt = min(total, kTsCap);
-  for (int i = tid; i < cnt; i += kFinT) {
-    ls[i] = ts_cs[q * kTsCap + i];
-    li[i] = ts_ci[q * kTsCap + i];
+#if MQ_FIN_DBG & 16
+  unsigned long long tsx[8];
+  tsx[0] = wall_clock64();
+#define MQ_FIN_TS(i) tsx[i] = wall_clock64()
+#else
+#define MQ_FIN_TS(i)
+#endif
+  if (MQ_FIN_DBG & 4) {
+    if (tid == 0) fail[atomicAdd(n_fail, 1)] = q;
+    return;
   }
-  if (tid < kc) {
-    cs[tid] = tau[q];
-    ci[tid] = -1;
-    sc[tid] = -INFINITY;
-    sid[tid] = -1;
-  }
-  if (wave == 3) {  // the bound, alongside the survivor loads
+  const int total = (MQ_FIN_DBG & 8) ? 0 : count[q];
+  const bool ranked = total <= kFinMaxSurv;  // block-uniform
+  const int cnt = ranked ? total : 0;
+  if (wave == 0) {  // ||q|| and the global bound
+    const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
+    float ss = 0.f;
+    for (int i = lane; i < (dim >> 2); i += 64) {
+      const floatx4 v = q4[i];
+      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
     const float E = screen_bound(Q, dim, q, VERIFY_BF16_Q32, stats, lane);
     if (lane == 0) {
       e_sh = E;
+      qn_sh = sqrtf(ss);
       ek_sh = -INFINITY;
+      lk_sh = -INFINITY;
+      nlive_sh = 0;
     }
   }
   __syncthreads();
-  for (int i = tid; i < cnt; i += kFinT) {
-    const float x = ls[i];
-    const int xi = li[i];
-    if (MQ_FIN_DBG & 1) {
-      if (i < kc) {
-        cs[i] = x;
-        ci[i] = xi;
+  MQ_FIN_TS(1);
+  {
+    // E_r as screen_bound forms E, with d = ||c_r - scale_r r8_r|| (x 1.001 slack, as the maxima)
+    const float qn = qn_sh, cmax = __uint_as_float(stats[1]) * 1.001f;
+    const float g = 2.f * (float)dim * 5.9604645e-8f;
+    for (int i = tid; i < cnt; i += kFinT) {
+      const float x = ts_cs[q * kTsCap + i];
+      const int xi = ts_ci[q * kTsCap + i];
+      const float d = err8[xi] * 1.001f;
+      const float Er = (qn * d + g * qn * (cmax + d) + g * qn * cmax) * 1.001f + 1e-7f;
+      lo[i] = x - Er;
+      ls[i] = x + Er;
+      li[i] = xi;
+    }
+    if (tid < ((cnt + 3) & ~3) - cnt) {
+      lo[cnt + tid] = -INFINITY;
+      li[cnt + tid] = INT_MAX;
+    }
+  }
+  __syncthreads();
+  MQ_FIN_TS(2);
+  // L_k: the survivor of rank k - 1 by (lo desc, id asc).  Each wave pops its k best
+  // (lanes hold survivors tid and tid + kFinT, keys (ord(lo), ~id): larger is better, all
+  // distinct), then the 8k wave winners are ranked against each other (the all-pairs rank
+  // of every survivor cost ~13 us at 320).  Fewer than k survivors leave -inf (every
+  // survivor live, and the certificate fails below)
+  if (!(MQ_FIN_DBG & 1)) {
+    auto fkey = [&](int i) -> unsigned long long {
+      return i < cnt ? ((unsigned long long)fin_ord(lo[i]) << 32) | (unsigned)~li[i] : 0ull;
+    };
+    unsigned long long a = fkey(tid), b = fkey(tid + kFinT);
+    if (b > a) {
+      const unsigned long long t = a;
+      a = b;
+      b = t;
+    }
+    for (int r = 0; r < k; ++r) {
+      const unsigned hi = wave_max_u32((unsigned)(a >> 32));
+      const unsigned lw = wave_max_u32((unsigned)(a >> 32) == hi ? (unsigned)a : 0u);
+      const unsigned long long m = ((unsigned long long)hi << 32) | lw;
+      if (lane == 0) wk[wave * k + r] = m;
+      if (a == m && m != 0ull) {
+        a = b;
+        b = 0ull;
       }
-      continue;
     }
+  }
+  __syncthreads();
+  if (tid < kFinW * k) {
+    const unsigned long long x = wk[tid];
     int rank = 0;
-#pragma unroll 8
-    for (int j = 0; j < cnt; ++j) rank += better(ls[j], li[j], x, xi) ? 1 : 0;
-    if (rank < kc) {
-      cs[rank] = rank == kc - 1 && total > kTsCap ? INFINITY : x;
-      ci[rank] = xi;
-    }
+#pragma unroll 4
+    for (int j = 0; j < kFinW * k; ++j) rank += wk[j] > x ? 1 : 0;
+    if (rank == k - 1 && x != 0ull) lk_sh = fin_unord((unsigned)(x >> 32));
   }
   __syncthreads();
-  if (wave == 0) {
-    int live = kc;
-    if (k < kc) {
-      const float cut = cs[k - 1] - 2.f * e_sh;
-      live = max(k, __popcll(__ballot(lane < kc && !(cs[lane] < cut))) + (kc > 64 ? kc - 64 : 0));
+  MQ_FIN_TS(3);
+  const float lk = lk_sh;
+  for (int i = tid; i < cnt; i += kFinT)
+    if (!(ls[i] < lk)) {
+      const int j = atomicAdd(&nlive_sh, 1);
+      if (j < kFinLive) lv[j] = i;
     }
-    if (lane == 0) live_sh = live;
-  }
   __syncthreads();
-  const int kl = live_sh;
+  MQ_FIN_TS(4);
+  const int nl = min(nlive_sh, kFinLive);
+  if (tid < ((nl + 3) & ~3) - nl) {
+    sc[nl + tid] = -INFINITY;
+    sid[nl + tid] = INT_MAX;
+  }
   const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
   constexpr int U = 8;  // eight candidates per wave per round (rerank_kernel's arithmetic): 64 per round
   const int slot = rerank_slot(lane);
-  for (int c0 = wave * U; c0 < kl; c0 += kFinW * U) {
+  for (int c0 = wave * U; c0 < nl; c0 += kFinW * U) {
     long long id[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) id[u] = c0 + u < kl ? ci[c0 + u] : -1;
+    for (int u = 0; u < U; ++u) id[u] = c0 + u < nl ? li[lv[c0 + u]] : -1;
     const float dot = (MQ_FIN_DBG & 2) ? 0.f : rerank_dots8(q4, rows, dim, id, lane);
     long long my_id = id[0];
 #pragma unroll
     for (int u = 1; u < U; ++u) my_id = slot == u ? id[u] : my_id;
-    if ((lane & 7) == 0 && c0 + slot < kl) {
-      sc[c0 + slot] = my_id >= 0 ? dot : -INFINITY;
-      sid[c0 + slot] = my_id;
+    if ((lane & 7) == 0 && c0 + slot < nl) {
+      sc[c0 + slot] = dot;  // (the live ids are real rows)
+      sid[c0 + slot] = (int)my_id;
     }
   }
   __syncthreads();
-  if (tid < kc) {
-    int rank = 0;
-    for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
+  MQ_FIN_TS(5);
+  for (int t = tid; t < nl; t += kFinT) {
+    const int rank = lds_rank4(sc4, sid4, (nl + 3) >> 2, sc[t], sid[t]);
     if (rank < k) {
-      const float x = sid[tid] >= 0 ? sc[tid] : -INFINITY;
-      os[q * k + rank] = x;
-      oi[q * k + rank] = sid[tid];
-      if (rank == k - 1) ek_sh = x;
+      os[q * k + rank] = sc[t];
+      oi[q * k + rank] = sid[t];
+      if (rank == k - 1) ek_sh = sc[t];
     }
   }
+  if (tid >= nl && tid < k) {  // fewer live rows than k: padding (and no certificate)
+    os[q * k + tid] = -INFINITY;
+    oi[q * k + tid] = -1;
+  }
   __syncthreads();
-  if (tid == 0 && !(cs[kc - 1] + e_sh < ek_sh)) fail[atomicAdd(n_fail, 1)] = q;
+  MQ_FIN_TS(6);
+  if (tid == 0) {
+    const bool cert = ranked && nlive_sh <= kFinLive && nl >= k && tau[q] + e_sh < ek_sh;
+    if (!cert) fail[atomicAdd(n_fail, 1)] = q;
+#if MQ_FIN_DBG & 16
+    printf("FIN cnt %d nl %d dt %llu %llu %llu %llu %llu %llu\n", cnt, nl, tsx[1] - tsx[0], tsx[2] - tsx[1],
+           tsx[3] - tsx[2], tsx[4] - tsx[3], tsx[5] - tsx[4], tsx[6] - tsx[5]);
+#endif
+  }
+#undef MQ_FIN_TS
 }
 
 // ======================================================= K10: merge lists ======
@@ -1106,7 +1222,7 @@ struct mq_index {
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   bool thresh_scan = true;  // batched bf16 screens use the threshold scan (K9t)
   DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t / K9q: sample maxima, tau, survivors
-  DevBuf rows8, scale8, stats8;  // int8 shadow [cap, dim] + per-row scales + its maxima (as stats16)
+  DevBuf rows8, scale8, err8, stats8;  // int8 shadow [cap, dim] + per-row scales, errors ||c - scale r8|| + maxima (as stats16)
   int64_t n8 = 0;                // rows already mirrored into rows8
   bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
   double i8_fail_avg = 0.0;      // running share of single queries the int8 screen failed to certify
@@ -1408,13 +1524,14 @@ int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, i
 int ensure_i8(mq_index* ix, hipStream_t s) {
   int rc = ix->rows8.ensure((size_t)(ix->cap + kI8PadRows) * ix->dim);
   if (!rc) rc = ix->scale8.ensure((size_t)(ix->cap + kI8PadRows) * sizeof(float));
+  if (!rc) rc = ix->err8.ensure((size_t)(ix->cap + kI8PadRows) * sizeof(float));
   if (!rc) rc = ix->stats8.ensure(2 * sizeof(unsigned));
   if (rc) return rc;
   if (ix->n8 < ix->n) {
     if (ix->n8 == 0) MQ_HIP(hipMemsetAsync(ix->stats8.p, 0, 2 * sizeof(unsigned), s));
     launch_i8_shadow(ix->rows + ix->n8 * ix->dim, ix->n - ix->n8, ix->dim,
                      ix->rows8.as<unsigned>() + ix->n8 * ix->dim / 4, ix->scale8.as<float>() + ix->n8,
-                     ix->stats8.as<unsigned>(), s);
+                     ix->err8.as<float>() + ix->n8, ix->stats8.as<unsigned>(), s);
     MQ_HIP(hipGetLastError());
     ix->n8 = ix->n;
   }
@@ -1438,7 +1555,7 @@ bool i8_ok(mq_index* ix, int64_t nq) {
 // K9q scans for nq = 1 query, then (os != null) the select of the top-kc candidates;
 // `zero` (optional) is set to 0 by the sample pass.  The timeline stays open (stage 1).
 int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t* oi, hipStream_t s,
-            int* zero = nullptr) {
+            int* zero = nullptr, int kcert = 0) {
   const size_t n_lists = (size_t)i8_lists(ix->num_cus);
   int rc = ensure_i8(ix, s);
   if (!rc) rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
@@ -1449,7 +1566,7 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   if (rc) return rc;
   ThreshI8Args a{q, (int)nq, ix->rows8.as<unsigned>(), ix->scale8.as<float>(), ix->n, ix->dim, ix->num_cus,
                  ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
-                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), zero};
+                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), zero, ix->stats8.as<unsigned>(), kcert};
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh_i8(a, s, &ix->tl);
   ix->tl.mark(s, 1);
@@ -1565,8 +1682,8 @@ bool x6_tier_ok(const mq_index* ix, int64_t nq, int k) {
 // 0.33 / 0.16 sigma (sigma = 0.036) apart at k = 5 / 16 / 32, and ~0.03 sigma at k = 50:
 // past k = 16 most certificates would fail and every batch would pay the screen AND the
 // re-run, so larger k goes straight to the split-f32 tier (bound 8e-5, kc = k + 8) or the
-// direct exact scan.
-constexpr int kScreenMaxK = 16;
+// direct exact scan.  (kScreenMaxK = 16 is defined with the K9q finish, which sizes its
+// wave winners by it.)
 constexpr double kBfSkipShare = 0.2;  // bf16 certificate failure share that disables the tier
 constexpr int kBfSkipSearches = 64;
 
@@ -1706,11 +1823,11 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     // scans (the sample pass zeroes the failure count), then select + re-rank + certificate
     // in one launch; the int8 screen's bound has the Q32 form (fp32 query) with the int8
     // shadow's maxima (kc = 64 < n: the int8 tier needs >= kTsMinRows rows)
-    rc = i8_topk(ix, q, nq, kc, nullptr, nullptr, s, ix->flag.as<int>());
+    rc = i8_topk(ix, q, nq, kc, nullptr, nullptr, s, ix->flag.as<int>(), k);
     if (rc) return rc;
     hipLaunchKernelGGL(i8_finish_kernel, dim3((unsigned)nq), dim3(kFinT), 0, s, q, ix->rows, ix->dim,
                        ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
-                       kc, k, ix->stats8.as<unsigned>(), os, oi, ix->flag.as<int>(), fail);
+                       k, ix->stats8.as<unsigned>(), ix->err8.as<float>(), os, oi, ix->flag.as<int>(), fail);
     ix->tl.close(s);
     MQ_HIP(hipGetLastError());
   } else {
@@ -1891,7 +2008,7 @@ int mq_index_destroy(mq_index* ix) {
     ix->flag.release();
     ix->stats16.release();
     for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->rows8,
-                      &ix->scale8, &ix->stats8})
+                      &ix->scale8, &ix->err8, &ix->stats8})
       b->release();
     ix->afb_q.release();
     ix->afb_cs.release();

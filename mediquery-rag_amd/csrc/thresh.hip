@@ -370,51 +370,62 @@ void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
 // multiplies, and one transposed butterfly (xor 32 / 16 / 8 halving the values, then
 // xor 4 / 2 / 1) leaves lane l with row 4 b5 + 2 b4 + b3 of the 8.
 
-// int8 shadow of rows [0, n) + scales + the screen statistics (float bits, atomicMax).
-// One wave per row; lane l quantises elements [l E, l E + E), E = 4 * E4.
+// int8 shadow of rows [0, n) + scales + per-row errors + the screen statistics (float bits,
+// atomicMax).  One wave per row, rows strided over a grid of a few waves per SIMD; lane l
+// quantises elements [l E, l E + E), E = 4 * E4.  Each wave keeps its running maxima and
+// issues one atomicMax pair at the end (one pair per row serialised ~1M same-address
+// atomics: 22.7 ms per 1M rows).
 template <int E4>
 __global__ __launch_bounds__(256) void i8_shadow_kernel(const float* __restrict__ src, int64_t n,
                                                         unsigned* __restrict__ r8,
                                                         float* __restrict__ scale,
+                                                        float* __restrict__ err,
                                                         unsigned* __restrict__ stats) {
   constexpr int E = 4 * E4, DIM = 64 * E;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n) return;
-  floatx4 x[E4];
-  float amax = 0.f;
+  float emax = 0.f, cmax = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    floatx4 x[E4];
+    float amax = 0.f;
 #pragma unroll
-  for (int d = 0; d < E4; ++d) {
-    x[d] = *reinterpret_cast<const floatx4*>(src + row * DIM + lane * E + 4 * d);
-    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x[d].x), fabsf(x[d].y)), fmaxf(fabsf(x[d].z), fabsf(x[d].w))));
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
-  const float sc = amax / 127.f, inv = amax > 0.f ? 127.f / amax : 0.f;
-  float se = 0.f, sd = 0.f;
-#pragma unroll
-  for (int d = 0; d < E4; ++d) {
-    unsigned w = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const float v = x[d][b];
-      const float r = fminf(fmaxf(rintf(v * inv), -127.f), 127.f);
-      const float deq = sc * r;
-      se += (v - deq) * (v - deq);
-      sd += deq * deq;
-      w |= ((unsigned)(int)r & 0xffu) << (8 * b);
+    for (int d = 0; d < E4; ++d) {
+      x[d] = *reinterpret_cast<const floatx4*>(src + row * DIM + lane * E + 4 * d);
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x[d].x), fabsf(x[d].y)), fmaxf(fabsf(x[d].z), fabsf(x[d].w))));
     }
-    r8[row * (DIM / 4) + lane * E4 + d] = w;
-  }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    se += __shfl_xor(se, off);
-    sd += __shfl_xor(sd, off);
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+    const float sc = amax / 127.f, inv = amax > 0.f ? 127.f / amax : 0.f;
+    float se = 0.f, sd = 0.f;
+#pragma unroll
+    for (int d = 0; d < E4; ++d) {
+      unsigned w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float v = x[d][b];
+        const float r = fminf(fmaxf(rintf(v * inv), -127.f), 127.f);
+        const float deq = sc * r;
+        se += (v - deq) * (v - deq);
+        sd += deq * deq;
+        w |= ((unsigned)(int)r & 0xffu) << (8 * b);
+      }
+      r8[row * (DIM / 4) + lane * E4 + d] = w;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      se += __shfl_xor(se, off);
+      sd += __shfl_xor(sd, off);
+    }
+    const float e = sqrtf(se);
+    if (lane == 0) {
+      scale[row] = sc;
+      err[row] = e;
+    }
+    emax = fmaxf(emax, e);
+    cmax = fmaxf(cmax, sqrtf(sd));
   }
-  if (lane == 0) {
-    scale[row] = sc;
-    atomicMax(stats, __float_as_uint(sqrtf(se)));
-    atomicMax(stats + 1, __float_as_uint(sqrtf(sd)));
+  if (lane == 0 && cmax > 0.f) {
+    atomicMax(stats, __float_as_uint(emax));
+    atomicMax(stats + 1, __float_as_uint(cmax));
   }
 }
 
@@ -427,6 +438,13 @@ __device__ __forceinline__ float key_ord(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+#ifndef MQ_I8_CERT_DBG  // measurement builds only: 1 = tau without the certificate term (r4's tau),
+                        // 2 = the certificate term computed, r4's tau kept
+#define MQ_I8_CERT_DBG 0
+#endif
+#if MQ_I8_CERT_DBG != 0 && !defined(MQ_MEASUREMENT_BUILD)
+#error "MQ_I8_CERT_DBG breaks the int8 certificate: only a measurement build (-DMQ_MEASUREMENT_BUILD) may set it"
+#endif
 #ifndef MQ_I8_ROWS
 #define MQ_I8_ROWS 8
 #endif
@@ -535,8 +553,10 @@ template <int E4, int NQ, int MODE>
 __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
     const float* __restrict__ Q, int nq, const unsigned* __restrict__ r8, const float* __restrict__ scale,
     int64_t n_rows, int64_t n_units, int period, float* __restrict__ tau, const float* __restrict__ lmax_in,
-    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci, int* __restrict__ zero) {
+    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci, int* __restrict__ zero,
+    const unsigned* __restrict__ stats, int kcert) {
   constexpr int E = 4 * E4, DIM = 64 * E;
+  if (MQ_I8_CERT_DBG & 1) kcert = 0;
   float* lmax = const_cast<float*>(lmax_in);  // written by TS_MAX, read by TS_APPEND
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -603,7 +623,12 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
   __shared__ float th_sh[NQ];
   const bool tau_wave = MODE == TS_APPEND && (threadIdx.x >> 6) == 0;
   unsigned key[NQ][kPer];
+  float st_d = 0.f, st_c = 0.f;  // the shadow's maxima (kcert > 0), loaded with the keys
   if (tau_wave) {
+    if (kcert > 0 && stats) {
+      st_d = __uint_as_float(stats[0]);
+      st_c = __uint_as_float(stats[1]);
+    }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -620,33 +645,66 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       for (int q = 0; q < NQ; ++q) {
 #if MQ_I8_TAU_POP
         // the kTsRank-th largest key (with multiplicity): each lane keeps its own top
-        // kTsRank keys (compare-exchange insertion), then kTsRank rounds of a wave max
-        // whose lowest holder pops its head - ~450 VALU instead of 32 rounds of kPer ballots
-        // (~4k instructions while the workgroup's other waves wait at the barrier).  Same T.
-        unsigned top[kTsRank];
+        // kPop keys (compare-exchange insertion), then rounds of a wave max whose lowest
+        // holder pops its head - ~450 VALU instead of 32 rounds of kPer ballots (~4k
+        // instructions while the workgroup's other waves wait at the barrier).  Same T.
+        // With kcert > 0 the pops run on to the kcert-th largest (Tk) as well.
+        constexpr int kPop = 16;  // >= kTsRank and >= the screens' k (kScreenMaxK)
+        unsigned top[kPop];
 #pragma unroll
-        for (int i = 0; i < kTsRank; ++i) top[i] = 0u;
+        for (int i = 0; i < kPop; ++i) top[i] = 0u;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
+          if (64 * j >= (int)gridDim.x) break;  // (uniform) lists past the grid: key 0
           unsigned x = key[q][j];
 #pragma unroll
-          for (int i = 0; i < kTsRank; ++i) {
+          for (int i = 0; i < kPop; ++i) {
             const unsigned hi = max(top[i], x);
             x = min(top[i], x);
             top[i] = hi;
           }
         }
-        unsigned T = 0;
-#pragma unroll
-        for (int r = 0; r < kTsRank; ++r) {
+        unsigned T = 0, Tk = 0, Tf = 0;
+        const int pops = kcert > 0 ? kPop : kTsRank;
+        for (int r = 0; r < pops; ++r) {
           const unsigned m = wave_max_u32(top[0]);
-          T = m;
+          if (r == kTsRank - 1) T = m;
+          if (r == kcert - 1) Tk = m;
+          if (r == kPop - 1) Tf = m;
           const unsigned long long holders = __ballot(top[0] == m);
-          if (r + 1 < kTsRank && lane == (int)__builtin_ctzll(holders)) {
+          if (r + 1 < pops && lane == (int)__builtin_ctzll(holders)) {
 #pragma unroll
-            for (int i = 0; i + 1 < kTsRank; ++i) top[i] = top[i + 1];
-            top[kTsRank - 1] = 0u;
+            for (int i = 0; i + 1 < kPop; ++i) top[i] = top[i + 1];
+            top[kPop - 1] = 0u;
           }
+        }
+        if (kcert > 0 && stats) {
+          // tau <= Tk - 2E: the kcert best sampled rows (one per top list) score >= Tk on
+          // the screen, so exact >= Tk - E each, hence e_k >= Tk - E > tau + E - the
+          // finish's certificate holds whenever every survivor is kept (the k-th best
+          // sample of a clustered query is a cluster-mate, its 8th list maximum too
+          // close to e_k: measured gaps ~0.01 against E ~0.013, tools/i8_cert_probe.py).  E as
+          // screen_bound(VERIFY_BF16_Q32) computes it (1% and 1e-6 slack for the
+          // different summation order of ||q||)
+          float ss = 0.f;
+#pragma unroll
+          for (int e = 0; e < E; ++e) ss += qv[q][e] * qv[q][e];
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+          const float qn = sqrtf(ss);
+          const float dmax = st_d * 1.001f, cmax = st_c * 1.001f;
+          const float g = 2.f * (float)DIM * 5.9604645e-8f;
+          const float Eb = (qn * dmax + g * qn * (cmax + dmax) + g * qn * cmax) * 1.001f + 1e-7f;
+          const float tk = Tk == 0u ? -INFINITY : key_ord(Tk);
+          const float tc = tk - 2.02f * Eb - 1e-6f;
+          const float t8 = T == 0u ? -INFINITY : key_ord(T);
+          // ... floored at the kPop-th largest maximum (>= 16 sampled rows: ~256 survivors
+          // expected), so a k-th best sample far below the true k-th best (k large against
+          // the query's cluster) cannot flood the survivor lists; then the certificate is
+          // no longer guaranteed, only likely
+          const float tf = Tf == 0u ? -INFINITY : key_ord(Tf);
+          const float t = fminf(t8, fmaxf(tc, tf));
+          T = (MQ_I8_CERT_DBG & 2) ? T : t == -INFINITY ? 0u : ord_key(t);
         }
 #else
         unsigned T = 0;
@@ -716,18 +774,20 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
 }
 
 template <int E4>
-void i8_shadow_e4(const float* rows, int64_t n, unsigned* r8, float* scale, unsigned* stats, hipStream_t s) {
-  hipLaunchKernelGGL((i8_shadow_kernel<E4>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rows, n, r8,
-                     scale, stats);
+void i8_shadow_e4(const float* rows, int64_t n, unsigned* r8, float* scale, float* err, unsigned* stats,
+                  hipStream_t s) {
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
+  if (grid == 0) return;
+  hipLaunchKernelGGL((i8_shadow_kernel<E4>), dim3(grid), dim3(256), 0, s, rows, n, r8, scale, err, stats);
 }
 
-void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, unsigned* stats,
-                      hipStream_t s) {
+void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, float* err,
+                      unsigned* stats, hipStream_t s) {
   switch (dim / 256) {
-    case 1: i8_shadow_e4<1>(rows, n, r8, scale, stats, s); break;
-    case 2: i8_shadow_e4<2>(rows, n, r8, scale, stats, s); break;
-    case 3: i8_shadow_e4<3>(rows, n, r8, scale, stats, s); break;
-    default: i8_shadow_e4<4>(rows, n, r8, scale, stats, s); break;
+    case 1: i8_shadow_e4<1>(rows, n, r8, scale, err, stats, s); break;
+    case 2: i8_shadow_e4<2>(rows, n, r8, scale, err, stats, s); break;
+    case 3: i8_shadow_e4<3>(rows, n, r8, scale, err, stats, s); break;
+    default: i8_shadow_e4<4>(rows, n, r8, scale, err, stats, s); break;
   }
 }
 
@@ -739,9 +799,9 @@ void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
   const int64_t n_units = (a.n + kI8Rows - 1) / kI8Rows;
   tl->mark(s, 0);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_MAX>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8, a.scale,
-                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero);
+                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero, a.stats, 0);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_APPEND>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8,
-                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr);
+                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr, a.stats, a.k);
 }
 
 void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,

@@ -56,6 +56,12 @@ struct ThreshI8Args {
   float* cs;                  // [nq][kTsCap] survivor scores
   int* ci;                    // [nq][kTsCap] survivor rows
   int* zero;                  // optional int the sample pass sets to 0 (the caller's fail count)
+  // the certificate's tau (index.hip i8_finish_kernel): with the shadow's maxima `stats`
+  // and the query's k, tau = min(the kTsRank-th largest sample list maximum, max(the k-th
+  // largest - 2E, the 16th largest)), E the screen's bound - tau + E < e_k then holds by
+  // construction unless the floor applies
+  const unsigned* stats = nullptr;
+  int k = 0;                  // 0: tau = the kTsRank-th largest maximum only
 };
 int i8_lists(int num_cus);
 // The sample and appending passes: survivors in cs / ci / count, tau in tau.
@@ -63,9 +69,10 @@ void launch_thresh_i8(const ThreshI8Args& a, hipStream_t s, Timeline* tl);
 // Survivors -> top-kc candidates per query (K9t's select; slots past the count: (tau, -1)).
 void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,
                    float* out_s, int64_t* out_i, hipStream_t s);
-// int8 shadow of rows [0, n): r8 [n][dim] int8, scale [n], stats [0] max ||c - scale r8||,
-// [1] max ||scale r8|| (float bits; atomicMax - zero them before the first rows).
-void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, unsigned* stats,
-                      hipStream_t s);
+// int8 shadow of rows [0, n): r8 [n][dim] int8, scale [n], err [n] = ||c - scale r8|| per
+// row, stats [0] max ||c - scale r8||, [1] max ||scale r8|| (float bits; atomicMax - zero
+// them before the first rows).
+void launch_i8_shadow(const float* rows, int64_t n, int dim, unsigned* r8, float* scale, float* err,
+                      unsigned* stats, hipStream_t s);
 
 }  // namespace mq

@@ -26,7 +26,7 @@ CUS = 256
 
 
 def short(name):
-    return name.split("(")[0].strip()
+    return name.replace("(anonymous namespace)::", "").split("(")[0].strip()
 
 
 def find(d, suffix):
@@ -79,7 +79,14 @@ def classify(rows):
     prev = ""
     for did, k, grid, v in rows:
         cls = None
-        if re.search(EXACT_GEMM + r"0" + LN_ARG, k):
+        mx = re.search(X6P_GEMM, k)
+        if mx:  # the split-f32 encoder GEMMs on pre-split weights (K2p)
+            e = mx.group(1)
+            cls = {"0": "qkv_gemm_x6p", "1": "ffn_up_gemm_x6p", "2": "ffn_up_gemm_x6p"}.get(e)
+            if e == "3":
+                cls = "out_proj_gemm_x6p" if "attention" in prev else \
+                    "ffn_down_gemm_x6p" if ("gemm_x6p_kernel" in prev or "gemm_nt_kernel" in prev) else None
+        elif re.search(EXACT_GEMM + r"0" + LN_ARG, k):
             cls = "qkv_gemm"
         elif re.search(EXACT_GEMM + r"[12]" + LN_ARG, k):
             cls = "ffn_up_gemm"
@@ -110,6 +117,8 @@ def mean(v):
 # the exact-f32 encoder GEMM (X6 = false, BF16 = false, optional slice-depth parameter)
 # followed by its epilogue id
 EXACT_GEMM = r"gemm_nt_kernel<mq::F32Tile<\d+, \d+, \d+, \d+, false, \d+, false(, \d+)?>, "
+# the split-f32 GEMM on pre-split weights (gemm_x6p.hip), its epilogue id captured
+X6P_GEMM = r"gemm_x6p_kernel<mq::X6pTile<[^>]*>, (\d)>"
 # ... then gemm_nt_kernel's LN_IN argument (r4: LayerNorm on load, false by default)
 LN_ARG = r"(, (true|false))?>"
 # bench.py kernel class -> kernel-name regex (the encoder GEMM classes are resolved per
