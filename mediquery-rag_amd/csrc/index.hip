@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
                                                         const float* __restrict__ rows, int dim,
                                                         const float* __restrict__ ts_cs,
                                                         const int* __restrict__ ts_ci,
-                                                        const int* __restrict__ count,
+                                                        const int* __restrict__ count, int lists,
                                                         const float* __restrict__ tau, int k,
                                                         const unsigned* __restrict__ stats,
                                                         const float* __restrict__ err8,
@@ -618,7 +618,8 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
   float* sc = reinterpret_cast<float*>(sc4);
   int* sid = reinterpret_cast<int*>(sid4);
   __shared__ float e_sh, qn_sh, ek_sh, lk_sh;
-  __shared__ int nlive_sh;
+  __shared__ int nlive_sh, ovf_sh;
+  __shared__ int wsum[kFinW];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if MQ_FIN_DBG & 16
@@ -632,8 +633,36 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
     if (tid == 0) fail[atomicAdd(n_fail, 1)] = q;
     return;
   }
-  const int total = (MQ_FIN_DBG & 8) ? 0 : count[q];
-  const bool ranked = total <= kFinMaxSurv;  // block-uniform
+  // the survivors' segments (one per scan workgroup, thresh.hpp kI8Seg): thread t owns
+  // segments t and t + kFinT; an exclusive scan of their counts places them
+  static_assert(kI8MaxLists <= 2 * kFinT, "two segments per thread");
+  int c0 = 0, c1 = 0;
+  if (!(MQ_FIN_DBG & 8)) {
+    c0 = tid < lists ? count[q * lists + tid] : 0;
+    c1 = tid + kFinT < lists ? count[q * lists + tid + kFinT] : 0;
+  }
+  const bool seg_ovf = c0 > kI8Seg || c1 > kI8Seg;
+  c0 = min(c0, kI8Seg);
+  c1 = min(c1, kI8Seg);
+  int incl = c0 + c1;  // inclusive scan: waves, then the wave totals
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  if (tid == 0) ovf_sh = 0;
+  __syncthreads();
+  if (seg_ovf) ovf_sh = 1;
+  int base = 0;
+#pragma unroll
+  for (int w = 0; w < kFinW; ++w) base += w < wave ? wsum[w] : 0;
+  int total = 0;
+#pragma unroll
+  for (int w = 0; w < kFinW; ++w) total += wsum[w];
+  const int beg = base + incl - c0 - c1;
+  __syncthreads();
+  const bool ranked = total <= kFinMaxSurv && ovf_sh == 0;  // block-uniform
   const int cnt = ranked ? total : 0;
   if (wave == 0) {  // ||q|| and the global bound
     const floatx4* q4 = reinterpret_cast<const floatx4*>(Q + q * dim);
@@ -659,14 +688,15 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
     // E_r as screen_bound forms E, with d = ||c_r - scale_r r8_r|| (x 1.001 slack, as the maxima)
     const float qn = qn_sh, cmax = __uint_as_float(stats[1]) * 1.001f;
     const float g = 2.f * (float)dim * 5.9604645e-8f;
-    for (int i = tid; i < cnt; i += kFinT) {
-      const float x = ts_cs[q * kTsCap + i];
-      const int xi = ts_ci[q * kTsCap + i];
+    for (int j = 0; ranked && j < c0 + c1; ++j) {
+      const int64_t at = (q * lists + (j < c0 ? tid : tid + kFinT)) * kI8Seg + (j < c0 ? j : j - c0);
+      const float x = ts_cs[at];
+      const int xi = ts_ci[at];
       const float d = err8[xi] * 1.001f;
       const float Er = (qn * d + g * qn * (cmax + d) + g * qn * cmax) * 1.001f + 1e-7f;
-      lo[i] = x - Er;
-      ls[i] = x + Er;
-      li[i] = xi;
+      lo[beg + j] = x - Er;
+      ls[beg + j] = x + Er;
+      li[beg + j] = xi;
     }
     if (tid < ((cnt + 3) & ~3) - cnt) {
       lo[cnt + tid] = -INFINITY;
@@ -1222,6 +1252,7 @@ struct mq_index {
   int stream_max_q = 4;  // batches up to this size use the streaming kernel (K9s)
   bool thresh_scan = true;  // batched bf16 screens use the threshold scan (K9t)
   DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t / K9q: sample maxima, tau, survivors
+  DevBuf i8c_cs, i8c_ci, i8c_count;  // K9q survivors compacted (the debug select path)
   DevBuf rows8, scale8, err8, stats8;  // int8 shadow [cap, dim] + per-row scales, errors ||c - scale r8|| + maxima (as stats16)
   int64_t n8 = 0;                // rows already mirrored into rows8
   bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
@@ -1560,9 +1591,12 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   int rc = ensure_i8(ix, s);
   if (!rc) rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
   if (!rc) rc = ix->ts_tau.ensure(nq * sizeof(float));
-  if (!rc) rc = ix->ts_count.ensure(nq * sizeof(int));
-  if (!rc) rc = ix->ts_cs.ensure((size_t)nq * kTsCap * sizeof(float));
-  if (!rc) rc = ix->ts_ci.ensure((size_t)nq * kTsCap * sizeof(int));
+  if (!rc) rc = ix->ts_count.ensure(nq * n_lists * sizeof(int));
+  if (!rc) rc = ix->ts_cs.ensure((size_t)nq * n_lists * kI8Seg * sizeof(float));
+  if (!rc) rc = ix->ts_ci.ensure((size_t)nq * n_lists * kI8Seg * sizeof(int));
+  if (!rc && os) rc = ix->i8c_count.ensure(nq * sizeof(int));
+  if (!rc && os) rc = ix->i8c_cs.ensure((size_t)nq * kTsCap * sizeof(float));
+  if (!rc && os) rc = ix->i8c_ci.ensure((size_t)nq * kTsCap * sizeof(int));
   if (rc) return rc;
   ThreshI8Args a{q, (int)nq, ix->rows8.as<unsigned>(), ix->scale8.as<float>(), ix->n, ix->dim, ix->num_cus,
                  ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
@@ -1570,8 +1604,12 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh_i8(a, s, &ix->tl);
   ix->tl.mark(s, 1);
-  if (os) launch_select(ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
-                        (int)nq, kc, os, oi, s);
+  if (os) {
+    launch_i8_compact(ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), (int)n_lists, (int)nq,
+                      ix->i8c_cs.as<float>(), ix->i8c_ci.as<int>(), ix->i8c_count.as<int>(), s);
+    launch_select(ix->i8c_cs.as<float>(), ix->i8c_ci.as<int>(), ix->i8c_count.as<int>(), ix->ts_tau.as<float>(),
+                  (int)nq, kc, os, oi, s);
+  }
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -1826,8 +1864,8 @@ int search_screened(mq_index* ix, int tier, const float* q, int64_t nq, int k, f
     rc = i8_topk(ix, q, nq, kc, nullptr, nullptr, s, ix->flag.as<int>(), k);
     if (rc) return rc;
     hipLaunchKernelGGL(i8_finish_kernel, dim3((unsigned)nq), dim3(kFinT), 0, s, q, ix->rows, ix->dim,
-                       ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(), ix->ts_tau.as<float>(),
-                       k, ix->stats8.as<unsigned>(), ix->err8.as<float>(), os, oi, ix->flag.as<int>(), fail);
+                       ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), ix->ts_count.as<int>(),
+                       i8_lists(ix->num_cus), ix->ts_tau.as<float>(), k, ix->stats8.as<unsigned>(), ix->err8.as<float>(), os, oi, ix->flag.as<int>(), fail);
     ix->tl.close(s);
     MQ_HIP(hipGetLastError());
   } else {
@@ -2007,7 +2045,8 @@ int mq_index_destroy(mq_index* ix) {
     ix->coarse_i.release();
     ix->flag.release();
     ix->stats16.release();
-    for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->rows8,
+    for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->i8c_cs,
+                      &ix->i8c_ci, &ix->i8c_count, &ix->rows8,
                       &ix->scale8, &ix->err8, &ix->stats8})
       b->release();
     ix->afb_q.release();

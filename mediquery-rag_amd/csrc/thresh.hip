@@ -580,9 +580,9 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
     th[q] = 0.f;
     mx[q] = -INFINITY;
   }
-  if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x < NQ) count[threadIdx.x] = 0;
   if (MODE == TS_MAX && blockIdx.x == 0 && threadIdx.x == 0 && zero) *zero = 0;  // caller's flag
   const int my_r = i8_row(lane);
+  __shared__ int seg_n[NQ];  // TS_APPEND: this workgroup's survivors per query
   const int64_t stride = (int64_t)W * period;
   unsigned a[kI8Stages][kI8Rows][E4];
   float sc[kI8Stages];
@@ -604,10 +604,11 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       if (MODE == TS_MAX) {
         mx[q] = valid ? fmaxf(mx[q], score) : mx[q];
       } else if ((lane & (64 / kI8Rows - 1)) == 0 && valid && q < nq && score >= th[q]) {
-        const int slot = atomicAdd(count + q, 1);
-        if (slot < kTsCap) {
-          cs[(int64_t)q * kTsCap + slot] = score;
-          ci[(int64_t)q * kTsCap + slot] = (int)row;
+        const int slot = atomicAdd(&seg_n[q], 1);  // LDS
+        if (slot < kI8Seg) {
+          const int64_t at = ((int64_t)q * gridDim.x + blockIdx.x) * kI8Seg + slot;
+          cs[at] = score;
+          ci[at] = (int)row;
         }
       }
     }
@@ -655,13 +656,14 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
         for (int i = 0; i < kPop; ++i) top[i] = 0u;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-          if (64 * j >= (int)gridDim.x) break;  // (uniform) lists past the grid: key 0
-          unsigned x = key[q][j];
+          if (64 * j < (int)gridDim.x) {  // (uniform) lists past the grid hold key 0
+            unsigned x = key[q][j];
 #pragma unroll
-          for (int i = 0; i < kPop; ++i) {
-            const unsigned hi = max(top[i], x);
-            x = min(top[i], x);
-            top[i] = hi;
+            for (int i = 0; i < kPop; ++i) {
+              const unsigned hi = max(top[i], x);
+              x = min(top[i], x);
+              top[i] = hi;
+            }
           }
         }
         unsigned T = 0, Tk = 0, Tf = 0;
@@ -723,6 +725,7 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
         }
       }
     }
+    if (threadIdx.x < NQ) seg_n[threadIdx.x] = 0;
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) th[q] = th_sh[q];
@@ -754,6 +757,10 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
       consume(s2, u + 2 * stride);
       u += 3 * stride;
     }
+  }
+  if (MODE == TS_APPEND) {  // the segment counts
+    __syncthreads();
+    if (threadIdx.x < nq) count[threadIdx.x * gridDim.x + blockIdx.x] = seg_n[threadIdx.x];
   }
   if (MODE == TS_MAX) {  // workgroup maxima: one list per workgroup (a shorter tau pass)
     __shared__ float wmax[4][NQ];
@@ -802,6 +809,41 @@ void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
                      a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero, a.stats, 0);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_APPEND>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8,
                      a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr, a.stats, a.k);
+}
+
+// K9q segments -> compact (one block per query, thread t owns segment t)
+__global__ __launch_bounds__(kI8MaxLists) void i8_compact_kernel(const float* __restrict__ cs,
+                                                                const int* __restrict__ ci,
+                                                                const int* __restrict__ count, int lists,
+                                                                float* __restrict__ out_cs,
+                                                                int* __restrict__ out_ci,
+                                                                int* __restrict__ out_count) {
+  __shared__ int off[kI8MaxLists];
+  __shared__ int ovf;
+  const int q = blockIdx.x, t = threadIdx.x;
+  const int c = t < lists ? count[q * lists + t] : 0;
+  if (t == 0) ovf = 0;
+  off[t] = min(c, kI8Seg);
+  __syncthreads();
+  if (c > kI8Seg) ovf = 1;
+  for (int d = 1; d < kI8MaxLists; d <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= d ? off[t - d] : 0;
+    __syncthreads();
+    off[t] += v;
+    __syncthreads();
+  }
+  const int end = off[t], beg = end - min(c, kI8Seg);
+  for (int j = beg; j < end && j < kTsCap; ++j) {
+    out_cs[(int64_t)q * kTsCap + j] = cs[((int64_t)q * lists + t) * kI8Seg + j - beg];
+    out_ci[(int64_t)q * kTsCap + j] = ci[((int64_t)q * lists + t) * kI8Seg + j - beg];
+  }
+  if (t == kI8MaxLists - 1) out_count[q] = ovf ? kTsCap + 1 : end;
+}
+
+void launch_i8_compact(const float* cs, const int* ci, const int* count, int lists, int nq, float* out_cs,
+                       int* out_ci, int* out_count, hipStream_t s) {
+  hipLaunchKernelGGL(i8_compact_kernel, dim3(nq), dim3(kI8MaxLists), 0, s, cs, ci, count, lists, out_cs, out_ci,
+                     out_count);
 }
 
 void launch_select(const float* cs, const int* ci, const int* count, const float* tau, int nq, int kc,

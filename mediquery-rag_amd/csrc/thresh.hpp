@@ -42,6 +42,11 @@ constexpr int kI8WgPerCu = MQ_I8_WG;   // 256-thread workgroups per CU (= reside
                                 // scan loops are persistent, a non-resident 4th would run late)
 constexpr int kI8MaxLists = 1024;  // workgroups per launch = sample lists (tau is found in-kernel)
 constexpr int kI8PadRows = 16;  // the shadow is allocated to whole 8- or 16-row units
+// Survivors of the appending pass: per query, one segment of kI8Seg slots per workgroup
+// (list), filled through an LDS counter with plain stores; the workgroup stores its count
+// at the end.  A single global counter made every append a returning atomic to memory
+// behind the streaming loads (~13 us for 320 survivors: the appending wave stalls).
+constexpr int kI8Seg = 16;
 struct ThreshI8Args {
   const float* q;             // fp32 queries [nq][dim]
   int nq;                     // 1
@@ -52,9 +57,9 @@ struct ThreshI8Args {
   int num_cus;
   float* lmax;                // [nq][i8_lists(num_cus)] sample-pass workgroup maxima
   float* tau;                 // [nq]
-  int* count;                 // [nq]
-  float* cs;                  // [nq][kTsCap] survivor scores
-  int* ci;                    // [nq][kTsCap] survivor rows
+  int* count;                 // [nq][lists] survivors per segment (may exceed kI8Seg: overflow)
+  float* cs;                  // [nq][lists][kI8Seg] survivor scores
+  int* ci;                    // [nq][lists][kI8Seg] survivor rows
   int* zero;                  // optional int the sample pass sets to 0 (the caller's fail count)
   // the certificate's tau (index.hip i8_finish_kernel): with the shadow's maxima `stats`
   // and the query's k, tau = min(the kTsRank-th largest sample list maximum, max(the k-th
@@ -64,6 +69,10 @@ struct ThreshI8Args {
   int k = 0;                  // 0: tau = the kTsRank-th largest maximum only
 };
 int i8_lists(int num_cus);
+// K9q segments -> a compact list per query (out_count = the survivors, kTsCap + 1 if a
+// segment overflowed; entries past kTsCap dropped), for launch_select
+void launch_i8_compact(const float* cs, const int* ci, const int* count, int lists, int nq, float* out_cs,
+                       int* out_ci, int* out_count, hipStream_t s);
 // The sample and appending passes: survivors in cs / ci / count, tau in tau.
 void launch_thresh_i8(const ThreshI8Args& a, hipStream_t s, Timeline* tl);
 // Survivors -> top-kc candidates per query (K9t's select; slots past the count: (tau, -1)).
