@@ -84,8 +84,11 @@ def encoder_flops(cfg, B, L):
 def cpu_baseline(args, cfg, corpus_host_fn):
     """Oracle (torch-CPU restatement) timed on this host: q/s = batch /
     (median of 5 encoder batches + median of 5 fp32 mm/topk batches over the full
-    corpus), after one warm-up batch each; p50 single query = median over 20 single
-    queries of encoder + search (bounded: ~20 s of CPU work in all)."""
+    corpus), after one warm-up batch each; p50 single query = median over 100 single
+    queries of encoder + search.  BASELINE.md §3's other configs as bounded legs beside
+    it (`configs`): config 2 (100k rows) measured whole; config 4 (10M rows, batch 1024)
+    and config 5 (1M bf16 rows, k = 50 re-rank) timed on a stated sample and scaled
+    linearly in rows / queries (~40 s of CPU work in all)."""
     from oracle.encoder import OracleEncoder
     from oracle.flat import search_fp32_torch
     from mediquery_hip.weights import synthetic_state_dict
@@ -93,7 +96,7 @@ def cpu_baseline(args, cfg, corpus_host_fn):
     torch.set_num_threads(threads)
     enc = OracleEncoder(cfg, synthetic_state_dict(cfg, 0))
     ids, mask = synth.token_batch(args.batch, args.seq_len)
-    reps, singles = 5, 20
+    reps, singles = 5, 100
     q = enc.embed(ids, mask)  # warm-up batch
     t_enc = []
     for _ in range(reps):
@@ -101,23 +104,67 @@ def cpu_baseline(args, cfg, corpus_host_fn):
         q = enc.embed(ids, mask)
         t_enc.append(time.perf_counter() - t0)
     c = corpus_host_fn()
-    search_fp32_torch(q, c, args.k, threads)  # warm-up batch
-    t_search = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        search_fp32_torch(q, c, args.k, threads)
-        t_search.append(time.perf_counter() - t0)
+
+    def med_search(qq, cc, k, n):
+        search_fp32_torch(qq, cc, k, threads)  # warm-up
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            search_fp32_torch(qq, cc, k, threads)
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    ts = med_search(q, c, args.k, reps)
     lat = []
     for j in range(singles + 2):
+        jj = j % args.batch
         t0 = time.perf_counter()
-        q1 = enc.embed(ids[j:j + 1], mask[j:j + 1])
+        q1 = enc.embed(ids[jj:jj + 1], mask[jj:jj + 1])
         search_fp32_torch(q1, c, args.k, threads)
         if j >= 2:
             lat.append((time.perf_counter() - t0) * 1e3)
-    te, ts = statistics.median(t_enc), statistics.median(t_search)
+    te = statistics.median(t_enc)
+    configs = {}
+    # config 2: 100k x 768, batch 256 embed + search (the first 100k rows of the same slab)
+    ts2 = med_search(q, c[:100_000], args.k, reps)
+    configs["config2"] = {"value": round(args.batch / (te + ts2), 2), "unit": "queries/s",
+                          "sample": "whole config: encoder median (above) + median of %d searches of %d "
+                                    "queries over 100000 rows (%.4f s)" % (reps, args.batch, ts2)}
+    # config 4: 10M rows, batch 1024 - 1024 queries over the slab, scaled in rows; encoder x4
+    q4 = np.concatenate([q] * 4)
+    ts4 = med_search(q4, c, args.k, 1)
+    scale4 = 10_000_000 / c.shape[0]
+    configs["config4"] = {"value": round(1024 / (4 * te + scale4 * ts4), 2), "unit": "queries/s",
+                          "sample": "1024 queries over the %d-row slab (%.3f s, one timed after a warm-up) "
+                                    "scaled x%.0f to 10M rows; encoder = 4 x the 256-query batch median"
+                                    % (c.shape[0], ts4, scale4)}
+    # config 5: bf16 coarse scan (torch bf16 mm) for 64 candidates + fp32 re-rank -> k = 50,
+    # search only (as the GPU line) - on the first 100k rows, scaled x10 to 1M
+    c5 = torch.as_tensor(np.asarray(c[:100_000], dtype=np.float32))
+    c5b = c5.to(torch.bfloat16)
+    qt = torch.as_tensor(np.asarray(q, dtype=np.float32))
+
+    def c5_search():
+        _, cand = torch.topk((qt.to(torch.bfloat16) @ c5b.T).float(), 64, dim=1)
+        ex = torch.einsum("qd,qkd->qk", qt, c5[cand])
+        v, o = torch.topk(ex, 50, dim=1)
+        return v, torch.gather(cand, 1, o)
+
+    c5_search()
+    t5 = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        c5_search()
+        t5.append(time.perf_counter() - t0)
+    ts5 = statistics.median(t5)
+    configs["config5"] = {"value": round(args.batch / (10 * ts5), 2), "unit": "queries/s (search only)",
+                          "sample": "median of 3: %d queries, torch bf16 mm over 100000 bf16 rows -> top-64 "
+                                    "-> fp32 re-rank -> k=50 (%.4f s), scaled x10 to 1M rows"
+                                    % (args.batch, ts5)}
     return {"value": round(args.batch / (te + ts), 2), "unit": "queries/s",
             "cores": threads, "kind": "port",
             "p50_single_query_ms": round(statistics.median(lat), 2),
+            "configs": configs,
             "sample": ("oracle torch-CPU fp32 on %d threads: median of %d %d-layer BERT encodes of %d "
                        "queries (L=%d) + median of %d fp32 mm+topk batches of %d queries over %d x 768 "
                        "rows (enc %.3f s/batch, search %.3f s/batch); p50 of %d single queries "
