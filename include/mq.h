@@ -157,9 +157,17 @@ int mq_index_data(mq_index* ix, void** device_rows);
  * [1] K10 merge; it synchronises on the recorded events and resets the counters. */
 int mq_index_set_timing(mq_index* ix, int enabled);
 int mq_index_read_timing(mq_index* ix, float* ms, int n);
-/* Persistence: a flat binary slab (header + rows), see DESIGN.md. */
+/* Persistence: a flat binary slab (header + rows); written files are
+ * fsync'ed before the call returns. */
 int mq_index_save(mq_index* ix, const char* path);
 int mq_index_load(mq_index* ix, const char* path);
+/* Append-only persistence (the store's segments): save_rows writes rows
+ * [row0, row0 + n) as a slab file of n rows; load_append appends a slab file's rows after
+ * the index's own, bit-identical (no re-normalisation).  Replace the whole-slab rewrite
+ * of Chroma's persist on every add (src/ingest_medical.py:106-110 and
+ * src/medical_engine.py:52 share the persist directory). */
+int mq_index_save_rows(mq_index* ix, const char* path, int64_t row0, int64_t n);
+int mq_index_load_append(mq_index* ix, const char* path);
 
 /* Host-side k-way merge of per-shard candidate lists (the step after the RCCL
  * all-gather).  scores/ids are [n_lists, nq, k_in] (list-major, as an

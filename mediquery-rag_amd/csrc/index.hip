@@ -11,6 +11,8 @@
 #include <memory>
 #include <vector>
 
+#include <unistd.h>
+
 #include "common.hpp"
 #include "gemm_f32.hpp"
 #include "thresh.hpp"
@@ -2357,41 +2359,36 @@ int mq_index_read_timing(mq_index* ix, float* ms, int n) {
   return MQ_OK;
 }
 
-int mq_index_save(mq_index* ix, const char* path) {
-  clear_error();
-  MQ_CHECK_ARG(ix && path, "NULL argument");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  DeviceGuard dg(ix->device);
+// rows [row0, row0 + n) as a slab file (header + rows), flushed to stable storage
+static int save_rows(mq_index* ix, const char* path, int64_t row0, int64_t n) {
   FILE* f = fopen(path, "wb");
   if (!f) MQ_FAIL(MQ_EIO, "cannot open %s for writing", path);
   FileHeader h;
   memcpy(h.magic, kMagic, 8);
   h.dim = ix->dim;
   h.dtype = ix->dtype;
-  h.n_rows = ix->n;
+  h.n_rows = n;
   bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
   const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (ix->dim * 4));
   std::vector<float> buf;
-  for (int64_t r0 = 0; ok && r0 < ix->n; r0 += chunk) {
-    const int64_t nr = std::min(chunk, ix->n - r0);
+  for (int64_t r0 = 0; ok && r0 < n; r0 += chunk) {
+    const int64_t nr = std::min(chunk, n - r0);
     buf.resize((size_t)nr * ix->dim);
-    if (hipMemcpy(buf.data(), ix->rows + r0 * ix->dim, buf.size() * 4, hipMemcpyDeviceToHost) !=
+    if (hipMemcpy(buf.data(), ix->rows + (row0 + r0) * ix->dim, buf.size() * 4, hipMemcpyDeviceToHost) !=
         hipSuccess) {
       fclose(f);
       MQ_FAIL(MQ_EHIP, "device->host copy failed while saving");
     }
     ok = fwrite(buf.data(), 4, buf.size(), f) == buf.size();
   }
+  ok = ok && fflush(f) == 0 && fsync(fileno(f)) == 0;
   ok = (fclose(f) == 0) && ok;
   if (!ok) MQ_FAIL(MQ_EIO, "short write to %s", path);
   return MQ_OK;
 }
 
-int mq_index_load(mq_index* ix, const char* path) {
-  clear_error();
-  MQ_CHECK_ARG(ix && path, "NULL argument");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  DeviceGuard dg(ix->device);
+// the rows of slab file `path` placed at row `at` (0: replace the index, ix->n: append)
+static int load_rows(mq_index* ix, const char* path, bool append) {
   FILE* f = fopen(path, "rb");
   if (!f) MQ_FAIL(MQ_EIO, "cannot open %s", path);
   FileHeader h;
@@ -2404,10 +2401,17 @@ int mq_index_load(mq_index* ix, const char* path) {
     MQ_FAIL(MQ_EINVAL, "%s holds dim %d dtype %d, index has dim %d dtype %d", path, h.dim, h.dtype,
             ix->dim, ix->dtype);
   }
-  ix->n = 0;
-  ix->n16 = 0;
-  ix->n8 = 0;
-  int rc = reserve_rows(ix, h.n_rows, nullptr);
+  const int64_t at = append ? ix->n : 0;
+  if (at + h.n_rows >= (int64_t)INT32_MAX) {
+    fclose(f);
+    MQ_FAIL(MQ_EINVAL, "index limited to 2^31-1 rows");
+  }
+  if (!append) {
+    ix->n = 0;
+    ix->n16 = 0;
+    ix->n8 = 0;
+  }
+  int rc = reserve_rows(ix, at + h.n_rows, nullptr);
   if (rc) {
     fclose(f);
     return rc;
@@ -2421,15 +2425,49 @@ int mq_index_load(mq_index* ix, const char* path) {
       fclose(f);
       MQ_FAIL(MQ_EIO, "%s is truncated", path);
     }
-    if (hipMemcpy(ix->rows + r0 * ix->dim, buf.data(), buf.size() * 4, hipMemcpyHostToDevice) !=
+    if (hipMemcpy(ix->rows + (at + r0) * ix->dim, buf.data(), buf.size() * 4, hipMemcpyHostToDevice) !=
         hipSuccess) {
       fclose(f);
       MQ_FAIL(MQ_EHIP, "host->device copy failed while loading");
     }
   }
   fclose(f);
-  ix->n = h.n_rows;  // rows were normalised before they were saved
+  ix->n = at + h.n_rows;  // rows were normalised before they were saved (the shadows extend lazily)
   return MQ_OK;
+}
+
+int mq_index_save(mq_index* ix, const char* path) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  return save_rows(ix, path, 0, ix->n);
+}
+
+int mq_index_save_rows(mq_index* ix, const char* path, int64_t row0, int64_t n) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  MQ_CHECK_ARG(row0 >= 0 && n >= 0 && row0 + n <= ix->n, "rows [%lld, %lld) outside [0, %lld)",
+               (long long)row0, (long long)(row0 + n), (long long)ix->n);
+  DeviceGuard dg(ix->device);
+  return save_rows(ix, path, row0, n);
+}
+
+int mq_index_load(mq_index* ix, const char* path) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  return load_rows(ix, path, false);
+}
+
+int mq_index_load_append(mq_index* ix, const char* path) {
+  clear_error();
+  MQ_CHECK_ARG(ix && path, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  return load_rows(ix, path, true);
 }
 
 int mq_topk_merge_device(const float* scores, const int64_t* ids, int n_lists, int64_t nq,

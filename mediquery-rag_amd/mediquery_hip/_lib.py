@@ -79,6 +79,8 @@ SIGNATURES = {
     "mq_index_read_timing": (_I, [_P, _P, _I]),
     "mq_index_save": (_I, [_P, ctypes.c_char_p]),
     "mq_index_load": (_I, [_P, ctypes.c_char_p]),
+    "mq_index_save_rows": (_I, [_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
+    "mq_index_load_append": (_I, [_P, ctypes.c_char_p]),
     "mq_topk_merge_host": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P]),
     "mq_topk_merge_device": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P, _P]),
     "mq_encoder_create": (_I, [_I, ctypes.POINTER(BertConfigC), _PP]),

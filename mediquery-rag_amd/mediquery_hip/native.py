@@ -164,6 +164,14 @@ class FlatIndex:
     def load(self, path):
         _lib.call("mq_index_load", self._h, str(path).encode())
 
+    def save_rows(self, path, row0, n):
+        """Rows [row0, row0 + n) as a slab file of n rows (a store segment)."""
+        _lib.call("mq_index_save_rows", self._h, str(path).encode(), int(row0), int(n))
+
+    def load_append(self, path):
+        """Append a slab file's rows, bit-identical (no re-normalisation)."""
+        _lib.call("mq_index_load_append", self._h, str(path).encode())
+
 
 def merge_topk_host(scores, ids, k_out):
     """[n_lists, nq, k_in] candidate lists -> global top-k_out (score desc, id asc)."""

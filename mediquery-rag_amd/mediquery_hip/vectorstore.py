@@ -18,9 +18,17 @@ count min(k, candidates) exceeds it raises instead of truncating.  Errors raise 
 reference's retrieve_node does not catch either).
 
 Persistence: `mq_<collection>.json` (ids, documents, metadatas, and the name of the slab
-file) is the commit point; each write puts the rows in a fresh `mq_<collection>.<gen>.flat`
+file) is the base commit point; a full write (the first write, `delete`, an upsert that
+replaces rows, an explicit `persist()`) puts the rows in a fresh `mq_<collection>.<gen>.flat`
 and then atomically replaces the JSON, so a crash leaves either the old or the new store,
-never a slab/sidecar mismatch.  A directory that holds a stock Chroma database
+never a slab/sidecar mismatch.  A plain append (`add_texts` of new ids) is append-only: the
+new rows go to a segment `mq_<collection>@<gen>.seg.flat` (+ `.seg.json`, their ids,
+documents and metadatas), committed by atomically replacing the small manifest
+`mq_<collection>@tail.json` (the base slab it extends + the segment list), so one added
+document costs a few KB of writes instead of the whole slab and sidecar ('@' cannot occur
+in a collection name: no sibling collection's file can match).  Loading applies the
+manifest's segments when it names the loaded base; a full write supersedes them, and after
+MAX_SEGMENTS appends the next one compacts.  A directory that holds a stock Chroma database
 (`chroma.sqlite3`, written by the reference's ingest) but no sidecar is refused: it must be
 re-ingested with this store (`python src/ingest_medical.py` after the import swap).
 """
@@ -177,10 +185,12 @@ def _check_k(k, n_candidates):
 
 
 class HipChroma(VectorStoreBase):
-    _FILES = ("mq_%s.flat", "mq_%s.json")
+    _FILES = ("mq_%s.flat", "mq_%s.json", "mq_%s@tail.json")
     FOREIGN_DB = "chroma.sqlite3"  # what langchain_chroma / chromadb persist
     _GEN = re.compile(r"[0-9a-f]{12}\.flat")  # slab generation suffix (persist() writes it)
     STALE_SLAB_S = 3600  # an uncommitted slab this old is a crashed writer's leftover
+    _SEG = re.compile(r"[0-9a-f]{12}\.seg\.(flat|json)")  # segment files (after 'mq_<name>@')
+    MAX_SEGMENTS = 256  # appends between compactions
 
     def __init__(self, collection_name="langchain", embedding_function=None,
                  persist_directory=None, client_settings=None, collection_metadata=None,
@@ -203,6 +213,7 @@ class HipChroma(VectorStoreBase):
         self._index = None
         self._dim = dim
         self._slab_name = None
+        self._segments = []    # committed segments after the base: {"slab", "delta", "n_rows"}
         self._written = set()  # slabs this instance wrote that no commit of its own names now
         if persist_directory and os.path.exists(self._path(1)):
             self._load()
@@ -235,34 +246,64 @@ class HipChroma(VectorStoreBase):
         if self._auto_persist:
             self.persist()
 
+    @staticmethod
+    def _write_json(path, obj):
+        """Write + fsync `path` + ".tmp", then atomically rename it to `path`."""
+        tmp = path + ".tmp"
+        with open(tmp, "w", encoding="utf-8") as f:
+            json.dump(obj, f, ensure_ascii=False)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
     def persist(self):
-        """Write the store under persist_directory (crash-safe, see the module doc)."""
+        """Write the whole store under persist_directory (crash-safe, see the module doc);
+        supersedes (and deletes) the append segments."""
         if not self._persist_directory or self._index is None:
             return
         d = self._persist_directory
         os.makedirs(d, exist_ok=True)
         slab = "mq_%s.%s.flat" % (self._collection_name, uuid.uuid4().hex[:12])
         self._index.save(os.path.join(d, slab))
-        side = self._path(1)
-        tmp = side + ".tmp"
-        with open(tmp, "w", encoding="utf-8") as f:
-            json.dump({"dim": self._dim, "slab": slab, "n_rows": len(self._ids), "ids": self._ids,
-                       "documents": self._texts, "metadatas": self._metas,
-                       "collection_metadata": self._collection_metadata}, f, ensure_ascii=False)
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, side)  # the commit point
+        self._write_json(self._path(1), {  # the commit point
+            "dim": self._dim, "slab": slab, "n_rows": len(self._ids), "ids": self._ids,
+            "documents": self._texts, "metadatas": self._metas,
+            "collection_metadata": self._collection_metadata})
         replaced, self._slab_name = self._slab_name, slab
         if replaced:
             self._written.add(replaced)
+        for seg in self._segments:  # superseded: the manifest names the old base
+            self._written.update((seg["slab"], seg["delta"]))
+        self._segments = []
+        try:
+            os.remove(self._path(2))
+        except OSError:
+            pass
         self._remove_orphan_slabs()
 
+    def _persist_append(self, row0, m):
+        """Commit rows [row0, row0 + m), just appended, as one segment (module doc)."""
+        if not (self._auto_persist and self._persist_directory and self._index is not None):
+            return
+        if self._slab_name is None or len(self._segments) >= self.MAX_SEGMENTS:
+            return self.persist()
+        d = self._persist_directory
+        stem = "mq_%s@%s.seg" % (self._collection_name, uuid.uuid4().hex[:12])
+        seg = {"slab": stem + ".flat", "delta": stem + ".json", "n_rows": m}
+        self._index.save_rows(os.path.join(d, seg["slab"]), row0, m)
+        self._write_json(os.path.join(d, seg["delta"]), {
+            "ids": self._ids[row0:], "documents": self._texts[row0:], "metadatas": self._metas[row0:]})
+        self._write_json(self._path(2), {"base_slab": self._slab_name,  # the commit point
+                                         "segments": self._segments + [seg]})
+        self._segments.append(seg)
+
     def _own_slab(self, f):
-        """Is file name `f` a slab of THIS collection (not of 'name.x', whose slabs also
-        start with 'mq_name.')?  Its generated names and the legacy single-slab name."""
-        prefix = "mq_%s." % self._collection_name
+        """Is file name `f` a slab or segment file of THIS collection (not of 'name.x', whose
+        slabs also start with 'mq_name.')?  Its generated names and the legacy single-slab name."""
+        prefix, sprefix = "mq_%s." % self._collection_name, "mq_%s@" % self._collection_name
         return f == self._FILES[0] % self._collection_name or (
-            f.startswith(prefix) and self._GEN.fullmatch(f[len(prefix):]) is not None)
+            f.startswith(prefix) and self._GEN.fullmatch(f[len(prefix):]) is not None) or (
+            f.startswith(sprefix) and self._SEG.fullmatch(f[len(sprefix):]) is not None)
 
     def _remove_orphan_slabs(self):
         """After a commit: delete the slabs this instance replaced (the one it loaded or
@@ -275,8 +316,11 @@ class HipChroma(VectorStoreBase):
             side_mtime = os.path.getmtime(self._path(1))
         except OSError:
             return
+        live = {self._slab_name}
+        for seg in self._segments:
+            live.update((seg["slab"], seg["delta"]))
         for f in os.listdir(d):
-            if f == self._slab_name or not self._own_slab(f):
+            if f in live or not self._own_slab(f):
                 continue
             p = os.path.join(d, f)
             try:
@@ -304,6 +348,24 @@ class HipChroma(VectorStoreBase):
         if len(self._index) != len(self._ids):
             raise RuntimeError("persisted index (%d rows) and sidecar (%d ids) disagree"
                                % (len(self._index), len(self._ids)))
+        tail = None
+        if os.path.exists(self._path(2)):
+            with open(self._path(2), "r", encoding="utf-8") as f:
+                tail = json.load(f)
+        if tail and tail.get("base_slab") == self._slab_name:  # else superseded by a full write
+            d = self._persist_directory
+            for seg in tail["segments"]:
+                self._index.load_append(os.path.join(d, seg["slab"]))
+                with open(os.path.join(d, seg["delta"]), "r", encoding="utf-8") as f:
+                    delta = json.load(f)
+                self._ids += delta["ids"]
+                self._texts += delta["documents"]
+                self._metas += delta["metadatas"]
+                if len(self._index) != len(self._ids):
+                    raise RuntimeError("segment %s (%d rows) and its delta disagree"
+                                       % (seg["slab"], seg["n_rows"]))
+                self._segments.append(seg)
+                self._written.update((seg["slab"], seg["delta"]))  # superseded by the next full write
         self._reindex_host()
 
     def _embed_query(self, query):
@@ -355,7 +417,10 @@ class HipChroma(VectorStoreBase):
         self._id_row.update((i, base + j) for j, i in enumerate(ids))
         self._cols.append(metadatas)
         self._version += 1
-        self._persist()
+        if existing:  # rows were replaced: a full write (compaction)
+            self._persist()
+        else:
+            self._persist_append(base, len(ids))
 
     def delete(self, ids=None, _persist=True, **kwargs):
         if not ids or self._index is None:

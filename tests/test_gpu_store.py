@@ -94,12 +94,15 @@ def test_k_limit_and_crash_safe_persist(embeddings, docs, tmp_path):
     assert len(store.similarity_search("血糖", k=64)) == 64
     slabs = [f for f in os.listdir(db) if f.endswith(".flat")]
     assert len(slabs) == 1 and not any(f.endswith(".tmp") for f in os.listdir(db))
-    store.add_texts(["额外的文本"], metadatas=[{"title": "extra"}])
-    slabs2 = [f for f in os.listdir(db) if f.endswith(".flat")]
-    assert len(slabs2) == 1 and slabs2 != slabs          # new generation, old one removed
+    store.add_texts(["额外的文本"], metadatas=[{"title": "extra"}])  # append: base + one segment
+    assert sorted(f for f in os.listdir(db) if f.endswith(".flat") and ".seg." not in f) == slabs
     again = HipChroma(persist_directory=db, embedding_function=embeddings)
     assert len(again) == 155
     assert again.similarity_search("额外的文本", k=1)[0].metadata["title"] == "extra"
+    store.persist()  # a full write: new generation, old slab and the segment removed
+    slabs2 = [f for f in os.listdir(db) if f.endswith(".flat")]
+    assert len(slabs2) == 1 and slabs2 != slabs and not any(f.endswith(".tmp") for f in os.listdir(db))
+    assert len(HipChroma(persist_directory=db, embedding_function=embeddings)) == 155
 
     bulk_db = str(tmp_path / "bulk")
     bulk = HipChroma.from_documents(documents=docs[:10], embedding=embeddings,
@@ -158,7 +161,10 @@ def test_upsert_by_existing_id_replaces_row_and_persists(embeddings, docs, tmp_p
     s1 = [d.page_content for d in store.similarity_search(docs[3].page_content, k=5)]
     s2 = [d.page_content for d in again.similarity_search(docs[3].page_content, k=5)]
     assert s1 == s2
-    again.add_texts(["新增"], ids=["doc200"])  # a commit: replaced + stale slabs go
+    again.add_texts(["新增"], ids=["doc200"])  # an append: one segment, nothing swept
+    assert len([f for f in os.listdir(db) if f.endswith(".seg.flat")]) == 1
+    assert len(HipChroma(persist_directory=db, embedding_function=embeddings)) == 32
+    again.persist()  # a full write: the replaced + stale slabs and the superseded segment go
     assert sorted(f for f in os.listdir(db) if f.endswith(".flat")) == sorted([again._slab_name, young, sibling])
     assert len(HipChroma(persist_directory=db, embedding_function=embeddings)) == 32
 
@@ -181,3 +187,67 @@ def test_filtered_search_equals_oracle_on_allowed_rows(embeddings, docs):
         ref = exact_scores(qe, emb[allowed])[0]
         order = np.lexsort((allowed, -ref))[:5]
         assert [r for r, _ in got] == allowed[order].tolist(), f
+
+
+def test_append_only_persistence(embeddings, docs, tmp_path):
+    """add_texts of new ids writes one segment (rows + a delta of their documents) and
+    commits it by replacing the small manifest; the base slab and sidecar are untouched.
+    A reload applies the committed segments in order (rows bit-identical), ignores an
+    uncommitted segment and a manifest that names a superseded base; delete compacts into
+    a new base and drops the segments."""
+    db = str(tmp_path / "db")
+    ids = ["doc%03d" % i for i in range(30)]
+    store = HipChroma.from_documents(documents=docs[:30], embedding=embeddings, ids=ids, persist_directory=db)
+    side = os.path.join(db, "mq_langchain.json")
+    base_slab, side_bytes = store._slab_name, open(side, "rb").read()
+    store.add_texts([docs[40].page_content, docs[41].page_content], metadatas=[{"t": 40}, {"t": 41}],
+                    ids=["doc040", "doc041"])
+    store.add_texts([docs[42].page_content], metadatas=[{"t": 42}], ids=["doc042"])
+    assert open(side, "rb").read() == side_bytes and store._slab_name == base_slab
+    tail = json.load(open(os.path.join(db, "mq_langchain@tail.json")))
+    assert tail["base_slab"] == base_slab and [g["n_rows"] for g in tail["segments"]] == [2, 1]
+    # an uncommitted segment (a writer that crashed before the manifest) is not loaded
+    open(os.path.join(db, "mq_langchain@0123456789ab.seg.flat"), "wb").write(b"partial")
+    again = HipChroma(persist_directory=db, embedding_function=embeddings)
+    assert len(again) == 33 and again.get(ids=["doc041"])["metadatas"] == [{"t": 41}]
+    assert np.array_equal(again._index.get(), store._index.get())  # bit-identical rows
+    q = docs[41].page_content
+    assert [d.page_content for d in again.similarity_search(q, k=5)] == \
+        [d.page_content for d in store.similarity_search(q, k=5)]
+    assert again.similarity_search(q, k=1, filter={"t": 41})[0].page_content == q
+    # upsert of an existing id and delete compact: a new base, no segments
+    again.delete(["doc040"])
+    assert not os.path.exists(os.path.join(db, "mq_langchain@tail.json"))
+    assert [f for f in os.listdir(db) if f.endswith(".seg.flat")] == ["mq_langchain@0123456789ab.seg.flat"]
+    third = HipChroma(persist_directory=db, embedding_function=embeddings)
+    assert len(third) == 32 and third.get(ids=["doc040"])["ids"] == []
+    # a manifest that names a superseded base (another writer's full write won) is ignored
+    json.dump({"base_slab": base_slab, "segments": tail["segments"]},
+              open(os.path.join(db, "mq_langchain@tail.json"), "w"))
+    assert len(HipChroma(persist_directory=db, embedding_function=embeddings)) == 32
+
+
+def test_append_one_doc_to_1m_store_persists_fast(embeddings, tmp_path):
+    """adding one document to a 1M-row persisted store commits in
+    <= 50 ms (append-only segment + manifest; the whole-slab rewrite it replaces wrote
+    3 GB and a 1M-document sidecar)."""
+    db = str(tmp_path / "db")
+    rng = np.random.default_rng(5)
+    n = 1_000_000
+    emb = rng.standard_normal((n, 768), dtype=np.float32)
+    store = HipChroma(persist_directory=db, embedding_function=embeddings, auto_persist=False, _ingest=True)
+    store.add_embeddings(emb, ["d%d" % i for i in range(n)], [{} for _ in range(n)], ["id%d" % i for i in range(n)])
+    del emb
+    store.persist()
+    store._auto_persist = True
+    one = rng.standard_normal((1, 768), dtype=np.float32)
+    times = []
+    for j in range(5):
+        t0 = time.perf_counter()
+        store.add_embeddings(one, ["new%d" % j], [{"j": j}], ["new%d" % j])
+        times.append((time.perf_counter() - t0) * 1e3)
+    print("append_one_doc_ms_1m", [round(t, 2) for t in times])
+    assert sorted(times)[2] <= 50.0, times
+    again = HipChroma(persist_directory=db, embedding_function=embeddings)
+    assert len(again) == n + 5 and again.get(ids=["new3"])["metadatas"] == [{"j": 3}]
+
