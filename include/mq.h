@@ -157,6 +157,28 @@ int mq_index_data(mq_index* ix, void** device_rows);
  * [1] K10 merge; it synchronises on the recorded events and resets the counters. */
 int mq_index_set_timing(mq_index* ix, int enabled);
 int mq_index_read_timing(mq_index* ix, float* ms, int n);
+/* Filtered search (Chroma's `similarity_search(filter=...)`, src/medical_engine.py:52,
+ * the LangChain VectorStore surface): a row mask on the device, bit r % 32 of word r / 32
+ * set = row r allowed, built from the store's metadata columns by mq_mask_eval /
+ * mq_mask_combine (device pointers, async on stream), then one exact search over the
+ * allowed rows.  mq_mask_eval: bits (mode)= lut[codes[r]] for rows [0, n), codes[r] = -1
+ * (key absent) or >= n_lut - 1 read lut[n_lut - 1]; mq_mask_combine: dst (mode)= src,
+ * src NULL = all ones, MQ_MASK_CLEAR zeroes dst. */
+#define MQ_MASK_SET 0
+#define MQ_MASK_AND 1
+#define MQ_MASK_OR 2
+#define MQ_MASK_CLEAR 3
+int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut, uint32_t* bits, int mode,
+                 void* stream);
+int mq_mask_combine(uint32_t* dst, const uint32_t* src, int64_t n_words, int mode, void* stream);
+/* Exact top-k of one query over the allowed rows (same ranking and padding as
+ * mq_index_search; bits: a device mask of >= ceil(n / 32) words).  The int8 certified
+ * screen runs with the mask; an uncertified query is answered from the allowed rows
+ * gathered on the device (counted by mq_index_masked_gathers).  Synchronous. */
+int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32_t* bits, float* out_scores,
+                           int64_t* out_ids, int io_on_device, void* stream);
+int mq_index_masked_gathers(const mq_index* ix, int64_t* count);
+
 /* Persistence: a flat binary slab (header + rows); written files are
  * fsync'ed before the call returns. */
 int mq_index_save(mq_index* ix, const char* path);

@@ -59,6 +59,107 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   for (int i = lane; i < (dim >> 2); i += 64) d[i] = s[i];
 }
 
+// ============================================ row masks (filtered search) ======
+// A metadata condition over one column: codes[r] (-1 = key absent in row r) index a
+// per-distinct-value truth table lut (its last entry: absent); 64 rows per wave, one
+// ballot, lanes 0 / 32 write the two words.  mode: MQ_MASK_SET / AND / OR into bits.
+__global__ __launch_bounds__(256) void mask_eval_kernel(const int* __restrict__ codes, int64_t n,
+                                                        const unsigned char* __restrict__ lut, int n_lut,
+                                                        unsigned* __restrict__ bits, int mode) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool v = false;
+  if (r < n) {
+    const int c = codes[r];
+    v = lut[(c >= 0 && c < n_lut - 1) ? c : n_lut - 1] != 0;
+  }
+  const unsigned long long b = __ballot(v);
+  const int lane = threadIdx.x & 63;
+  if ((lane & 31) == 0 && r < n) {
+    const unsigned w = (unsigned)(lane ? b >> 32 : b);
+    unsigned* d = bits + (r >> 5);
+    *d = mode == MQ_MASK_AND ? (*d & w) : mode == MQ_MASK_OR ? (*d | w) : w;
+  }
+}
+
+// dst (op)= src; src == NULL: op MQ_MASK_SET fills ones, MQ_MASK_AND leaves dst;
+// MQ_MASK_CLEAR zeroes dst
+__global__ __launch_bounds__(256) void mask_combine_kernel(unsigned* __restrict__ dst,
+                                                           const unsigned* __restrict__ src,
+                                                           int64_t n_words, int mode) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_words) return;
+  const unsigned x = src ? src[w] : ~0u;
+  dst[w] = mode == MQ_MASK_AND ? (dst[w] & x) : mode == MQ_MASK_OR ? (dst[w] | x) : mode == MQ_MASK_CLEAR ? 0u : x;
+}
+
+// sorted compaction of the set bits of rows [0, n): pass 1 = per-block counts (256 words
+// per block), pass 2 = one block scans them (exclusive, in place; total in blk[nb]),
+// pass 3 = each block writes its rows in order
+__device__ __forceinline__ unsigned mask_word(const unsigned* bits, int64_t w, int64_t n) {
+  if (w * 32 >= n) return 0u;
+  const unsigned x = bits[w];
+  const int64_t rem = n - w * 32;
+  return rem >= 32 ? x : (x & ((1u << rem) - 1u));
+}
+__device__ __forceinline__ int block_excl_scan256(int v, int* sh, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) sh[wave] = incl;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) base += i < wave ? sh[i] : 0;
+  *total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return base + incl - v;
+}
+__global__ __launch_bounds__(256) void mask_count_kernel(const unsigned* __restrict__ bits, int64_t n,
+                                                         int* __restrict__ blk) {
+  __shared__ int sh[4];
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int total;
+  block_excl_scan256(__popc(mask_word(bits, w, n)), sh, &total);
+  if (threadIdx.x == 0) blk[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(256) void mask_scan_kernel(int* __restrict__ blk, int nb) {
+  __shared__ int sh[4];
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += 256) {
+    const int i = b0 + threadIdx.x;
+    const int v = i < nb ? blk[i] : 0;
+    int total;
+    const int ex = block_excl_scan256(v, sh, &total);
+    if (i < nb) blk[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) blk[nb] = carry;
+}
+__global__ __launch_bounds__(256) void mask_compact_kernel(const unsigned* __restrict__ bits, int64_t n,
+                                                           const int* __restrict__ blk,
+                                                           int64_t* __restrict__ rows) {
+  __shared__ int sh[4];
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned x = mask_word(bits, w, n);
+  int total;
+  int at = blk[blockIdx.x] + block_excl_scan256(__popc(x), sh, &total);
+  while (x) {
+    const int b = __builtin_ctz(x);
+    rows[at++] = w * 32 + b;
+    x &= x - 1u;
+  }
+}
+// result ids of the gathered sub-index -> store rows
+__global__ __launch_bounds__(256) void remap_ids_kernel(int64_t* __restrict__ ids, int64_t count,
+                                                        const int64_t* __restrict__ rows) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < count && ids[i] >= 0) ids[i] = rows[ids[i]];
+}
+
 // ================================================ K9: fused score + top-k ======
 // Search tile geometries: (WAVES_M, WAVES_N, TM, TN).
 using SearchWide = F32Tile<2, 2, 2, 2>;    // 128 queries x 128 rows per block
@@ -1255,8 +1356,12 @@ struct mq_index {
   bool thresh_scan = true;  // batched bf16 screens use the threshold scan (K9t)
   DevBuf ts_lmax, ts_tau, ts_count, ts_cs, ts_ci;  // K9t / K9q: sample maxima, tau, survivors
   DevBuf i8c_cs, i8c_ci, i8c_count;  // K9q survivors compacted (the debug select path)
+  DevBuf msel, mblk;     // masked search: the allowed rows (sorted) + per-block counts
+  DevBuf mres_s, mres_i;  // masked search: results staged for the host
+  mq_index* msub = nullptr;  // masked search fallback: the allowed rows gathered
   DevBuf rows8, scale8, err8, stats8;  // int8 shadow [cap, dim] + per-row scales, errors ||c - scale r8|| + maxima (as stats16)
   int64_t n8 = 0;                // rows already mirrored into rows8
+  int64_t masked_gathers = 0;    // masked searches the int8 screen could not certify (gathered)
   bool i8_screen = true;         // single queries screen on the int8 shadow first (K9q)
   double i8_fail_avg = 0.0;      // running share of single queries the int8 screen failed to certify
   int i8_skip = 0;               // searches left that bypass the int8 tier after a bad run
@@ -1588,7 +1693,7 @@ bool i8_ok(mq_index* ix, int64_t nq) {
 // K9q scans for nq = 1 query, then (os != null) the select of the top-kc candidates;
 // `zero` (optional) is set to 0 by the sample pass.  The timeline stays open (stage 1).
 int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t* oi, hipStream_t s,
-            int* zero = nullptr, int kcert = 0) {
+            int* zero = nullptr, int kcert = 0, const unsigned* mask = nullptr) {
   const size_t n_lists = (size_t)i8_lists(ix->num_cus);
   int rc = ensure_i8(ix, s);
   if (!rc) rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
@@ -1602,7 +1707,7 @@ int i8_topk(mq_index* ix, const float* q, int64_t nq, int kc, float* os, int64_t
   if (rc) return rc;
   ThreshI8Args a{q, (int)nq, ix->rows8.as<unsigned>(), ix->scale8.as<float>(), ix->n, ix->dim, ix->num_cus,
                  ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
-                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), zero, ix->stats8.as<unsigned>(), kcert};
+                 ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), zero, ix->stats8.as<unsigned>(), kcert, mask};
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh_i8(a, s, &ix->tl);
   ix->tl.mark(s, 1);
@@ -2047,8 +2152,9 @@ int mq_index_destroy(mq_index* ix) {
     ix->coarse_i.release();
     ix->flag.release();
     ix->stats16.release();
+    if (ix->msub) mq_index_destroy(ix->msub);
     for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->i8c_cs,
-                      &ix->i8c_ci, &ix->i8c_count, &ix->rows8,
+                      &ix->i8c_ci, &ix->i8c_count, &ix->msel, &ix->mblk, &ix->mres_s, &ix->mres_i, &ix->rows8,
                       &ix->scale8, &ix->err8, &ix->stats8})
       b->release();
     ix->afb_q.release();
@@ -2175,6 +2281,145 @@ int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst
   dst->n = n;
   dst->n16 = 0;
   dst->n8 = 0;
+  return MQ_OK;
+}
+
+// Filtered exact search of one query over the rows whose mask bit is set (Chroma's
+// similarity_search(filter=), src/medical_engine.py:52).  The int8 certified screen (K9q)
+// runs with the mask - masked rows do not exist for its sample, appending pass or
+// certificate, so the answer is exact over the allowed rows; a query it cannot certify
+// (or k > 16, or an index the int8 tier does not apply to) takes the gather path: the
+// allowed rows compacted in order on the device, gathered into a sub-index, scanned
+// exactly (direct fp32), ids mapped back.  Synchronous.
+int search_masked(mq_index* ix, const float* q, int k, const unsigned* bits, float* os, int64_t* oi,
+                  hipStream_t s) {
+  if (ix->n == 0) return fill_padding(os, oi, k, s);
+  const bool exact_kind = ix->precision == MQ_DTYPE_F32_SCREEN || ix->precision == MQ_DTYPE_F32;
+  if (exact_kind && k <= kScreenMaxK && ix->i8_screen && ix->dim % 256 == 0 && ix->dim <= 1024 &&
+      ix->n >= kTsMinRows && ix->n < (1ll << 31)) {
+    int rc = ix->flag.ensure(sizeof(int));
+    if (!rc) rc = ix->tier_fail[TIER_I8].ensure(sizeof(int64_t));
+    if (!rc) rc = i8_topk(ix, q, 1, MQ_MAX_K, nullptr, nullptr, s, ix->flag.as<int>(), k, bits);
+    if (rc) return rc;
+    hipLaunchKernelGGL(i8_finish_kernel, dim3(1), dim3(kFinT), 0, s, q, ix->rows, ix->dim, ix->ts_cs.as<float>(),
+                       ix->ts_ci.as<int>(), ix->ts_count.as<int>(), i8_lists(ix->num_cus), ix->ts_tau.as<float>(),
+                       k, ix->stats8.as<unsigned>(), ix->err8.as<float>(), os, oi, ix->flag.as<int>(),
+                       ix->tier_fail[TIER_I8].as<int64_t>());
+    ix->tl.close(s);
+    MQ_HIP(hipGetLastError());
+    int n_fail = 0;
+    rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);
+    if (rc) return rc;
+    if (n_fail == 0) return MQ_OK;
+    ix->masked_gathers++;
+  }
+  // gather path
+  const int64_t n_words = (ix->n + 31) / 32;
+  const int nb = (int)((n_words + 255) / 256);
+  int rc = ix->msel.ensure((size_t)ix->n * sizeof(int64_t));
+  if (!rc) rc = ix->mblk.ensure((size_t)(nb + 1) * sizeof(int));
+  if (rc) return rc;
+  int* blk = ix->mblk.as<int>();
+  hipLaunchKernelGGL(mask_count_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk);
+  hipLaunchKernelGGL(mask_scan_kernel, dim3(1), dim3(256), 0, s, blk, nb);
+  hipLaunchKernelGGL(mask_compact_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk, ix->msel.as<int64_t>());
+  MQ_HIP(hipGetLastError());
+  int count = 0;
+  rc = read_flag(ix, blk + nb, s, &count);
+  if (rc) return rc;
+  if (count == 0) return fill_padding(os, oi, k, s);
+  if (!ix->msub) {
+    rc = mq_index_create(ix->device, ix->dim, 0, ix->dtype, &ix->msub);
+    if (rc) return rc;
+  }
+  mq_index* sub = ix->msub;
+  sub->n = 0;  // (nothing of the previous filter's rows is kept)
+  rc = reserve_rows(sub, count, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((count + 3) / 4)), dim3(256), 0, s, ix->rows,
+                     ix->msel.as<int64_t>(), (int64_t)count, ix->dim, sub->rows);
+  MQ_HIP(hipGetLastError());
+  sub->n = count;
+  sub->n16 = sub->n8 = 0;
+  const int kk = (int)std::min<int64_t>(k, count);
+  if (kk < k) {
+    rc = fill_padding(os, oi, k, s);
+    if (rc) return rc;
+  }
+  rc = ix->out_s.ensure((size_t)k * 4);
+  if (!rc) rc = ix->out_i.ensure((size_t)k * 8);
+  if (rc) return rc;
+  // (kk results into scratch, then into the first kk slots)
+  rc = search_direct(sub, q, 1, kk, ix->out_s.as<float>(), ix->out_i.as<int64_t>(), s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(remap_ids_kernel, dim3(1), dim3(256), 0, s, ix->out_i.as<int64_t>(), (int64_t)kk,
+                     ix->msel.as<int64_t>());
+  MQ_HIP(hipGetLastError());
+  MQ_HIP(hipMemcpyAsync(os, ix->out_s.p, (size_t)kk * 4, hipMemcpyDeviceToDevice, s));
+  MQ_HIP(hipMemcpyAsync(oi, ix->out_i.p, (size_t)kk * 8, hipMemcpyDeviceToDevice, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut, uint32_t* bits, int mode,
+                 void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(n >= 0 && n_lut >= 1, "bad mask shape");
+  MQ_CHECK_ARG(mode == MQ_MASK_SET || mode == MQ_MASK_AND || mode == MQ_MASK_OR, "bad mask mode %d", mode);
+  if (n == 0) return MQ_OK;
+  MQ_CHECK_ARG(codes && lut && bits, "NULL buffer");
+  hipLaunchKernelGGL(mask_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const int*)codes, n, (const unsigned char*)lut, n_lut, (unsigned*)bits, mode);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_mask_combine(uint32_t* dst, const uint32_t* src, int64_t n_words, int mode, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(n_words >= 0, "negative word count");
+  MQ_CHECK_ARG(mode >= MQ_MASK_SET && mode <= MQ_MASK_CLEAR, "bad mask mode %d", mode);
+  if (n_words == 0) return MQ_OK;
+  MQ_CHECK_ARG(dst, "NULL dst");
+  hipLaunchKernelGGL(mask_combine_kernel, dim3((unsigned)((n_words + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (unsigned*)dst, (const unsigned*)src, n_words, mode);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32_t* bits, float* out_scores,
+                           int64_t* out_ids, int io_on_device, void* stream) {
+  clear_error();
+  MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(k >= 1 && k <= MQ_MAX_K, "k must be in [1, %d] (got %d)", MQ_MAX_K, k);
+  MQ_CHECK_ARG(query && bits && out_scores && out_ids, "NULL buffer");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (io_on_device) {
+    const int rc = search_masked(ix, query, k, (const unsigned*)bits, out_scores, out_ids, s);
+    if (rc) return rc;
+    MQ_HIP(hipStreamSynchronize(s));
+    return MQ_OK;
+  }
+  int rc = ix->stage.ensure((size_t)ix->dim * 4);
+  if (!rc) rc = ix->mres_s.ensure((size_t)k * 4);
+  if (!rc) rc = ix->mres_i.ensure((size_t)k * 8);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(ix->stage.p, query, (size_t)ix->dim * 4, hipMemcpyHostToDevice, s));
+  rc = search_masked(ix, ix->stage.as<float>(), k, (const unsigned*)bits, ix->mres_s.as<float>(),
+                     ix->mres_i.as<int64_t>(), s);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(out_scores, ix->mres_s.p, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(out_ids, ix->mres_i.p, (size_t)k * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipStreamSynchronize(s));
+  return MQ_OK;
+}
+
+int mq_index_masked_gathers(const mq_index* ix, int64_t* count) {
+  clear_error();
+  MQ_CHECK_ARG(ix && count, "NULL argument");
+  std::lock_guard<std::mutex> lk(const_cast<mq_index*>(ix)->mu);
+  *count = ix->masked_gathers;
   return MQ_OK;
 }
 

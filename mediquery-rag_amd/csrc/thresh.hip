@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
     const float* __restrict__ Q, int nq, const unsigned* __restrict__ r8, const float* __restrict__ scale,
     int64_t n_rows, int64_t n_units, int period, float* __restrict__ tau, const float* __restrict__ lmax_in,
     int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci, int* __restrict__ zero,
-    const unsigned* __restrict__ stats, int kcert) {
+    const unsigned* __restrict__ stats, int kcert, const unsigned* __restrict__ mask) {
   constexpr int E = 4 * E4, DIM = 64 * E;
   if (MQ_I8_CERT_DBG & 1) kcert = 0;
   float* lmax = const_cast<float*>(lmax_in);  // written by TS_MAX, read by TS_APPEND
@@ -586,18 +586,20 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
   const int64_t stride = (int64_t)W * period;
   unsigned a[kI8Stages][kI8Rows][E4];
   float sc[kI8Stages];
+  unsigned mw[kI8Stages];  // (mask) the word holding this lane's row's bit
   int64_t u = (int64_t)gw * period;
   auto fetch = [&](int buf, int64_t unit) {
     const int64_t uu = min(unit, n_units - 1);  // past the end: re-read the last unit
     i8_load<E4>(r8, uu, lane, a[buf]);
     sc[buf] = scale[uu * kI8Rows + my_r];  // (padding rows: allocated, unused)
+    mw[buf] = mask ? mask[(uu * kI8Rows + my_r) >> 5] : ~0u;  // (rows < 8 n_units <= 32 ceil(n / 32))
   };
   auto consume = [&](int buf, int64_t unit) {
     float v[kI8Rows * NQ];
     i8_dot<E4, NQ>(a[buf], qv, v);
     transpose_reduce<NQ>(v, lane);
     const int64_t row = unit * kI8Rows + my_r;
-    const bool valid = row < n_rows;
+    const bool valid = row < n_rows && ((mw[buf] >> (row & 31)) & 1u);  // masked rows do not exist
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const float score = v[q] * sc[buf];
@@ -806,9 +808,9 @@ void launch_i8_nq(const ThreshI8Args& a, hipStream_t s, Timeline* tl) {
   const int64_t n_units = (a.n + kI8Rows - 1) / kI8Rows;
   tl->mark(s, 0);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_MAX>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8, a.scale,
-                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero, a.stats, 0);
+                     a.n, n_units, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.zero, a.stats, 0, a.mask);
   hipLaunchKernelGGL((i8_thresh_kernel<E4, NQ, TS_APPEND>), dim3(G), dim3(256), 0, s, a.q, a.nq, a.r8,
-                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr, a.stats, a.k);
+                     a.scale, a.n, n_units, 1, a.tau, a.lmax, a.count, a.cs, a.ci, nullptr, a.stats, a.k, a.mask);
 }
 
 // K9q segments -> compact (one block per query, thread t owns segment t)

@@ -67,6 +67,9 @@ struct ThreshI8Args {
   // construction unless the floor applies
   const unsigned* stats = nullptr;
   int k = 0;                  // 0: tau = the kTsRank-th largest maximum only
+  // optional row mask (filtered search): bit r % 32 of word r / 32 set = row r exists;
+  // masked rows are skipped by both passes (>= ceil(n / 32) words)
+  const unsigned* mask = nullptr;
 };
 int i8_lists(int num_cus);
 // K9q segments -> a compact list per query (out_count = the survivors, kTsCap + 1 if a

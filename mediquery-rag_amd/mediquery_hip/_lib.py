@@ -20,6 +20,7 @@ MQ_DTYPE_F32, MQ_DTYPE_BF16, MQ_DTYPE_F32X6, MQ_DTYPE_F32_SCREEN = 0, 1, 2, 3
 MQ_GELU_ERF, MQ_GELU_TANH = 0, 1
 MQ_POOL_CLS, MQ_POOL_MEAN = 0, 1
 MQ_MAX_K = 64
+MQ_MASK_SET, MQ_MASK_AND, MQ_MASK_OR, MQ_MASK_CLEAR = 0, 1, 2, 3
 # mq_encoder_set_option ids (include/mq.h)
 MQ_ENC_OPT_ROWS_MAX, MQ_ENC_OPT_ROWS_SPLITS, MQ_ENC_OPT_SPLITK_MAX = 0, 1, 2
 MQ_ENC_OPT_LN_ROWS_PER_WAVE, MQ_ENC_OPT_FUSE_ATTN_OPROJ, MQ_ENC_OPT_FUSED_LN = 3, 4, 5
@@ -81,6 +82,10 @@ SIGNATURES = {
     "mq_index_load": (_I, [_P, ctypes.c_char_p]),
     "mq_index_save_rows": (_I, [_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
     "mq_index_load_append": (_I, [_P, ctypes.c_char_p]),
+    "mq_mask_eval": (_I, [_P, _I64, _P, _I, _P, _I, _P]),
+    "mq_mask_combine": (_I, [_P, _P, _I64, _I, _P]),
+    "mq_index_search_masked": (_I, [_P, _P, _I, _P, _P, _P, _I, _P]),
+    "mq_index_masked_gathers": (_I, [_P, ctypes.POINTER(_I64)]),
     "mq_topk_merge_host": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P]),
     "mq_topk_merge_device": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P, _P]),
     "mq_encoder_create": (_I, [_I, ctypes.POINTER(BertConfigC), _PP]),

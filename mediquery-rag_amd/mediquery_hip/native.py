@@ -164,6 +164,23 @@ class FlatIndex:
     def load(self, path):
         _lib.call("mq_index_load", self._h, str(path).encode())
 
+    def search_masked(self, query, k, bits):
+        """Exact top-k of one query over the rows allowed by `bits` (a device mask tensor of
+        >= ceil(n / 32) int32 words, bit r % 32 of word r / 32 = row r; mask_eval builds it)."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(self.dim)
+        scores = np.empty((1, k), dtype=np.float32)
+        ids = np.empty((1, k), dtype=np.int64)
+        _lib.call("mq_index_search_masked", self._h, _lib.ptr(q), k, _lib.ptr(bits), _lib.ptr(scores),
+                  _lib.ptr(ids), 0, _lib.stream_handle(None))
+        return scores, ids
+
+    @property
+    def masked_gathers(self):
+        """Masked searches the int8 screen did not certify (answered from gathered rows)."""
+        n = ctypes.c_int64()
+        _lib.call("mq_index_masked_gathers", self._h, ctypes.byref(n))
+        return n.value
+
     def save_rows(self, path, row0, n):
         """Rows [row0, row0 + n) as a slab file of n rows (a store segment)."""
         _lib.call("mq_index_save_rows", self._h, str(path).encode(), int(row0), int(n))
@@ -273,3 +290,17 @@ class Encoder:
         B, L = ids.shape
         _lib.call("mq_encoder_embed", self._h, _lib.ptr(ids), _lib.ptr(mask), B, L, _lib.ptr(out),
                   1, _lib.stream_handle(stream))
+
+
+def mask_eval(codes, lut, bits, mode, stream=None):
+    """bits (mode)= lut[codes] on the device (include/mq.h mq_mask_eval): codes int32 [n]
+    (-1 = key absent -> lut[-1]), lut uint8 [n_lut], bits int32 [ceil(n / 32)] (torch,
+    device)."""
+    _lib.call("mq_mask_eval", _lib.ptr(codes), codes.numel(), _lib.ptr(lut), lut.numel(), _lib.ptr(bits),
+              mode, _lib.stream_handle(stream))
+
+
+def mask_combine(dst, src, mode, stream=None):
+    """dst (mode)= src (None: all ones; MQ_MASK_CLEAR: zeros) on the device."""
+    _lib.call("mq_mask_combine", _lib.ptr(dst), _lib.ptr(src), dst.numel(), mode, _lib.stream_handle(stream))
+

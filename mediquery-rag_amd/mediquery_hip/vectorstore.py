@@ -42,7 +42,7 @@ import numpy as np
 
 from . import _lib
 from .compat import Document, VectorStoreBase
-from .native import FlatIndex
+from .native import FlatIndex, mask_combine, mask_eval
 
 DEFAULT_K = 4  # LangChain VectorStore.similarity_search default; the reference passes k=5
 
@@ -106,12 +106,16 @@ def _pred(op, v, x):
 class _MetaColumns:
     """Metadata held column-wise for vectorised Chroma `where` filters: per key, int32
     codes [n] (-1 = key absent in that row) into the key's distinct values.  A condition
-    is evaluated once per DISTINCT value (Python) and mapped onto the rows by numpy, so a
-    filter over 1M rows costs milliseconds; results equal `_match` row by row."""
+    is evaluated once per DISTINCT value (Python) into a truth table; the rows are mapped
+    through it on the device (`dmask`: mq_mask_eval over a device mirror of the codes,
+    a row bitmask the masked search reads) or by numpy (`mask`, for get()); results equal
+    `_match` row by row."""
 
     def __init__(self):
         self.n = 0
         self.cols = {}  # key -> [codes np.int32 (capacity >= n), values list, {hash key: code}]
+        self.ver = 0    # bumped by append / compact (device mirrors are per version)
+        self.dev = {}   # key -> (ver, device int32 codes [n])
 
     @staticmethod
     def _hkey(v):
@@ -141,12 +145,65 @@ class _MetaColumns:
                     col[1].append(v)
                 col[0][self.n + r] = code
         self.n = need
+        self.ver += 1
 
     def compact(self, keep):
         """Keep rows `keep` (sorted int64 row ids), in order."""
         for col in self.cols.values():
             col[0] = np.ascontiguousarray(col[0][:self.n][keep])
         self.n = len(keep)
+        self.ver += 1
+
+    @staticmethod
+    def _lut(values, op, x):
+        """Truth table of one condition over a column's distinct values (+ absent, last)."""
+        lut = np.zeros(len(values) + 1, np.uint8)
+        lut[-1] = _pred(op, None, x)
+        for cv, v in enumerate(values):
+            lut[cv] = _pred(op, v, x)
+        return lut
+
+    def dev_codes(self, key, dev):
+        got = self.dev.get(key)
+        if got is None or got[0] != self.ver:
+            import torch
+            got = self.dev[key] = (self.ver, torch.from_numpy(self.cols[key][0][:self.n]).to(dev))
+        return got[1]
+
+    def dmask(self, where, device):
+        """Row bitmask of `where` on the device (int32 words, bit r % 32 of word r / 32)."""
+        import torch
+        dev = torch.device("cuda", device)
+        bits = torch.empty(max(1, (self.n + 31) // 32), dtype=torch.int32, device=dev)
+        mask_combine(bits, None, _lib.MQ_MASK_SET)  # all rows
+        self._dapply(where, bits, dev)
+        return bits
+
+    def _dapply(self, where, bits, dev):
+        """bits &= where (the conditions of one dict are ANDed)."""
+        import torch
+        for key, cond in where.items():
+            if key == "$and":
+                for c in cond:
+                    self._dapply(c, bits, dev)
+            elif key == "$or":
+                acc, tmp = torch.empty_like(bits), torch.empty_like(bits)
+                mask_combine(acc, None, _lib.MQ_MASK_CLEAR)
+                for c in cond:
+                    mask_combine(tmp, None, _lib.MQ_MASK_SET)
+                    self._dapply(c, tmp, dev)
+                    mask_combine(acc, tmp, _lib.MQ_MASK_OR)
+                mask_combine(bits, acc, _lib.MQ_MASK_AND)
+            else:
+                col = self.cols.get(key)
+                ops = cond.items() if isinstance(cond, dict) else (("$eq", cond),)
+                for op, x in ops:
+                    if col is None:  # no row has the key
+                        if not _pred(op, None, x):
+                            mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
+                        continue
+                    lut = torch.from_numpy(self._lut(col[1], op, x)).to(dev)
+                    mask_eval(self.dev_codes(key, dev), lut, bits, _lib.MQ_MASK_AND)
 
     def mask(self, where):
         out = np.ones(self.n, bool)
@@ -167,11 +224,7 @@ class _MetaColumns:
                 for op, x in ops:
                     # admitted codes -> one table lookup per row; code -1 (key absent)
                     # indexes the table's last entry
-                    lut = np.zeros(len(values) + 1, bool)
-                    lut[-1] = _pred(op, None, x)
-                    for cv, v in enumerate(values):
-                        lut[cv] = _pred(op, v, x)
-                    out &= lut[codes]
+                    out &= self._lut(values, op, x).astype(bool)[codes]
         return out
 
 
@@ -207,9 +260,7 @@ class HipChroma(VectorStoreBase):
         self._ids, self._texts, self._metas = [], [], []
         self._id_row = {}              # id -> row (upsert / delete / get by id in O(1))
         self._cols = _MetaColumns()    # metadata column-wise, for vectorised filters
-        self._version = 0              # bumped by every write (filtered-search cache key)
-        self._scratch = None           # reused device index for filtered searches
-        self._scratch_key = None       # (filter, version) whose rows the scratch holds
+        self._version = 0              # bumped by every write
         self._index = None
         self._dim = dim
         self._slab_name = None
@@ -469,22 +520,16 @@ class HipChroma(VectorStoreBase):
             kk = _check_k(k, n)
             s, i = self._index.search(q, kk)
             return [(int(r), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
-        # exact filtered search: score only the allowed rows, gathered on the device into
-        # one reused scratch index (rows bit-identical to the store's); a repeated filter
-        # on an unchanged store reuses the gathered rows
-        key = (json.dumps(filter, sort_keys=True, default=repr), self._version)
-        if key != self._scratch_key:
-            allowed = np.flatnonzero(self._cols.mask(filter)).astype(np.int64)
-            if self._scratch is None:
-                self._scratch = FlatIndex(dim=self._dim, device=self._device)
-            self._index.select(allowed, out=self._scratch)
-            self._scratch_rows, self._scratch_key = allowed, key
-        allowed = self._scratch_rows
-        if len(allowed) == 0:
-            return []
-        kk = _check_k(k, len(allowed))
-        s, i = self._scratch.search(q, kk)
-        return [(int(allowed[r]), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
+        # exact filtered search on the device: the where-mask built from the device codes
+        # (mq_mask_eval), then the masked search (int8 certified screen with the mask, or
+        # the allowed rows gathered on the device); nothing row-sized crosses PCIe
+        if k > _lib.MQ_MAX_K:  # the result count decides between raising and returning all
+            k = _check_k(k, int(self._cols.mask(filter).sum()))
+            if k == 0:
+                return []
+        bits = self._cols.dmask(filter, self._device)
+        s, i = self._index.search_masked(q[0], int(k), bits)
+        return [(int(r), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
 
     def similarity_search_by_vector_with_score(self, embedding, k=DEFAULT_K, filter=None, **kwargs):
         return [(self._doc(r), max(0.0, 2.0 - 2.0 * c)) for r, c in self._search_rows(embedding, k, filter)]

@@ -1,0 +1,109 @@
+"""Device-side filtered search (Chroma's `similarity_search(filter=...)` on the VectorStore
+surface): the `where` mask is built on the device
+from the store's metadata code columns (mq_mask_eval / mq_mask_combine) and the masked
+search runs the int8 certified screen with masked rows absent, or gathers the allowed rows
+on the device.  Every answer against a float64 torch reference over exactly the rows
+`_match` admits (tie-group-aware check_topk), at 1M rows and at edge sizes."""
+import numpy as np
+import pytest
+
+from mediquery_hip import _lib, synth
+from mediquery_hip.native import FlatIndex, mask_combine, mask_eval
+from mediquery_hip.vectorstore import HipChroma, _match
+from oracle.flat import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(store, rows64, q, k, where, metas):
+    import torch
+    dev = rows64.device
+    allowed = np.array([r for r, m in enumerate(metas) if _match(m, where)], dtype=np.int64)
+    got = store._search_rows(q, k, where)
+    kk = min(k, len(allowed))
+    assert len(got) == kk, (where, len(got), kk)
+    if kk == 0:
+        return
+    al = torch.as_tensor(allowed, device=dev)
+    ref = (rows64[al] @ torch.as_tensor(q, dtype=torch.float64, device=dev)).cpu().numpy()
+    order = np.lexsort((allowed, -ref))
+    ids = np.array([[r for r, _ in got]])
+    sc = np.array([[c for _, c in got]], dtype=np.float32)
+    pos = {int(r): j for j, r in enumerate(allowed)}
+    fails = check_topk(ids, sc, None, kk,
+                       ref_top=(ref[order][None, :kk + 1], allowed[order][None, :kk + 1]), n_rows=len(rows64),
+                       ref_lookup=lambda b, rr: ref[[pos[int(x)] for x in rr]] if all(int(x) in pos for x in rr)
+                       else np.full(len(rr), -np.inf))
+    assert fails == [], (where, fails[:3])
+
+
+def test_mask_kernels_match_numpy(require_gpu):
+    """mq_mask_eval / mq_mask_combine against numpy, with ragged n (tail words)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    for n in (1, 31, 33, 64, 1000, 4097):
+        codes = rng.integers(-1, 5, n).astype(np.int32)
+        lut = rng.integers(0, 2, 6).astype(np.uint8)
+        lut2 = rng.integers(0, 2, 6).astype(np.uint8)
+        want = lut[np.where(codes >= 0, codes, 5)].astype(bool)
+        want2 = lut2[np.where(codes >= 0, codes, 5)].astype(bool)
+        w = (n + 31) // 32
+        bits = torch.empty(w, dtype=torch.int32, device=dev)
+        tmp = torch.empty_like(bits)
+        dc = torch.as_tensor(codes, device=dev)
+        mask_combine(bits, None, _lib.MQ_MASK_SET)
+        mask_eval(dc, torch.as_tensor(lut, device=dev), bits, _lib.MQ_MASK_AND)
+        mask_eval(dc, torch.as_tensor(lut2, device=dev), tmp, _lib.MQ_MASK_SET)
+        mask_combine(bits, tmp, _lib.MQ_MASK_OR)
+        got = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(got, want | want2), n
+        mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
+        assert int(bits.abs().sum()) == 0
+
+
+@pytest.fixture(scope="module")
+def big_store(require_gpu):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = 1_000_000
+    rows = synth.corpus_device(n, 768, dev)
+    metas = [{"src": int(i % 7), "year": int((i * 7919) % 50)} for i in range(n)]
+    metas[123456]["rare"] = "yes"
+    metas[654321]["rare"] = "yes"
+    store = HipChroma(dim=768, auto_persist=False)
+    store.add_embeddings(rows.cpu().numpy(), ["d%d" % i for i in range(n)], metas, ["id%d" % i for i in range(n)])
+    rows64 = torch.nn.functional.normalize(rows.double(), dim=1)
+    del rows
+    yield store, rows64, metas
+    del rows64
+
+
+@pytest.mark.parametrize("where,k", [
+    ({"src": 3}, 5),
+    ({"$or": [{"src": 1}, {"year": {"$gte": 40}}]}, 5),
+    ({"year": {"$lt": 1}}, 16),
+    ({"$and": [{"src": {"$in": [0, 2]}}, {"year": {"$ne": 7}}]}, 1),
+    ({"src": 3}, 20),              # k > 16: the gather path
+    ({"rare": "yes"}, 5),          # two rows: fewer than k, the gather path
+    ({"src": 99}, 5),              # no row
+    ({"missing_key": {"$ne": 1}}, 5),  # absent key: $ne admits every row
+])
+def test_filtered_search_1m_equals_fp64_over_allowed_rows(big_store, where, k):
+    store, rows64, metas = big_store
+    rng = np.random.default_rng(abs(hash(str(where))) % 2**31)
+    for j in range(3):
+        r = int(rng.integers(0, len(metas)))
+        q = rows64[r].float().cpu().numpy() + 0.02 * rng.standard_normal(768).astype(np.float32)
+        _check(store, rows64, q, k, where, metas)
+
+
+def test_wide_filters_certify_on_the_int8_screen(big_store):
+    """The masked int8 screen answers the wide filters itself (no gather)."""
+    store, rows64, metas = big_store
+    g0 = store._index.masked_gathers
+    rng = np.random.default_rng(11)
+    for j in range(20):
+        q = rows64[int(rng.integers(0, len(metas)))].float().cpu().numpy()
+        store._search_rows(q, 5, {"src": j % 7})
+    assert store._index.masked_gathers - g0 <= 2

@@ -1,8 +1,10 @@
 """Filtered vs unfiltered search latency at the VectorStore surface:
 `HipChroma.similarity_search_by_vector(q, k=5, filter=...)` over N synthetic rows whose
 metadata carries a 16-value `tag` and an integer `n`; the filter passes ~1/2 or ~1/16 of
-the rows.  Reports p50 ms for: no filter, a repeated filter (the gathered scratch index is
-reused), and a fresh filter every call (vectorised where-evaluation + device gather).
+the rows.  Reports p50 ms for: no filter, a repeated filter and a fresh filter every call
+(r5: the where-mask built on the device from the metadata code columns, then the masked
+int8 certified search; r3/r4 gathered the allowed rows through a host row list), and the
+masked searches that fell back to the device gather.
 
   python tools/filter_latency.py [--rows 1000000] [--iters 50]
 """
@@ -57,6 +59,7 @@ def main():
         lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"tag": "t%d" % (i % 16)}), args.iters)
     out["fresh_filter_half_ms"] = p50(
         lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"n": {"$lt": 40 + i % 20}}), args.iters)
+    out["masked_gathers"] = store._index.masked_gathers
     t0 = time.perf_counter()
     store.delete(["id%d" % i for i in range(0, n, 1000)])
     out["delete_1k_of_n_s"] = round(time.perf_counter() - t0, 3)
