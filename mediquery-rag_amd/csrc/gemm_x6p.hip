@@ -504,11 +504,11 @@ using X6p0 = X6pTile<2, 2, 2, 3, 4, 1, 4, true, 0, 1, 0, 6, true>;  // 128 x 192
 using X6p1 = X6pTile<4, 1, 2, 3, 4, 1, 4, true, 0, 1, 0, 6, true>;  // 256 x 96, same
 using X6p2 = X6pTile<4, 2, 1, 3, 4, 1, 4, true, 0, 2, 1, 6>;        // 128 x 192, 8 waves, DMAs from 0-3
 using X6p3 = X6pTile<4, 2, 2, 3, 4, 1, 8, true, 0, 6, 1, 8>;        // 256 x 192, 8 waves
-// measurement variants (tile codes 4-7)
+// measurement variants (tile codes 4-6; 7 is a product tile)
 using X6p4 = X6pTile<2, 2, 2, 3, 3, 2, 4, true, 0, 1, 0, 6, true>;  // tile 0 with 32-deep stages, 3 slots
 using X6p5 = X6pTile<2, 2, 2, 3, 4, 1, 4, true, 0, 1, 0, 4, true>;  // tile 0, split from slot 4
 using X6p6 = X6pTile<2, 2, 2, 3, 5, 1, 4, true, 0, 1, 0, 6, true>;  // tile 0 with 5 slots
-using X6p7 = X6pTile<2, 2, 2, 3, 4, 1, 4, true, 0, 1, 0, 10, true>; // tile 0, split from slot 10
+using X6p7 = X6pTile<2, 2, 1, 3, 4, 1, 4, true, 0, 1, 0, 6, true>;  // 64 x 192, loaders (product: out-proj)
 
 template <class T, int EPI>
 void launch_t(const X6pArgs& g, int num_cus, hipStream_t s) {
@@ -570,7 +570,15 @@ int x6p_pick_tile(int M, int N, int num_cus) {
 }
 
 void launch_gemm_x6p(const X6pArgs& g, int epi, int tile, int num_cus, hipStream_t s) {
-  if (tile < 0) tile = x6p_pick_tile(g.M, g.N, num_cus);
+  if (tile < 0) {
+    tile = x6p_pick_tile(g.M, g.N, num_cus);
+    // a short, narrow GEMM (out-proj: N = K = 768) that 128 x 192 covers in one round of
+    // one tile per CU runs 64 x 192 tiles, two per CU: the ring carries into the second
+    // tile, the first's epilogue overlaps its loads (57.2 vs 59.3 us at M = 8192; slower
+    // on the deeper and wider shapes, tools/gemm_x6p_bench.py)
+    const int64_t t0 = (int64_t)((g.M + 127) / 128) * ((g.N + 191) / 192);
+    if (g.K <= 768 && g.N <= 768 && t0 <= num_cus && t0 * 2 > num_cus) tile = 7;
+  }
   switch (epi) {
     case EPI_GELU_ERF: launch_tile<EPI_GELU_ERF>(g, tile, num_cus, s); return;
     case EPI_GELU_TANH: launch_tile<EPI_GELU_TANH>(g, tile, num_cus, s); return;

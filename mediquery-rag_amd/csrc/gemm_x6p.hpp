@@ -45,8 +45,10 @@ struct X6pArgs {
 
 // Tile shapes (workgroups of 8 waves, one per CU): 0 = 128 x 192 (4 compute + 4 loader
 // waves; the default: M = 8192 at N = 768 / 1536 / 2304 / 3072 gives whole rounds of 256
-// tiles), 1 = 256 x 96 (same waves), 2 = 128 x 192 and 3 = 256 x 192 (8 compute waves).
-// -1 = the pick below.
+// tiles), 1 = 256 x 96 (same waves), 2 = 128 x 192 and 3 = 256 x 192 (8 compute waves),
+// 7 = 64 x 192 (4 + 4 waves; out-proj-like shapes, see launch_gemm_x6p); 4-6 are
+// measurement variants of tile 0.  -1 = the pick below (+ tile 7 for N, K <= 768 when
+// 128 x 192 would run a single round).
 int x6p_pick_tile(int M, int N, int num_cus);
 // epi: EPI_BIAS / EPI_GELU_ERF / EPI_GELU_TANH / EPI_RESID (gemm_epi.hpp)
 void launch_gemm_x6p(const X6pArgs& g, int epi, int tile, int num_cus, hipStream_t s);
