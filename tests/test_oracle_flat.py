@@ -43,6 +43,18 @@ def test_checker_accepts_tie_permutations_and_rejects_errors():
     assert check_topk([[0, 1, 2]], [[0.9, 0.8, 0.81]], s, 3) != []    # score off by 1e-2
 
 
+def test_checker_tie_tolerance_stays_at_the_floor_for_accurate_scores():
+    """ADVICE r4: the tie group is max(1e-6, 3 e_b) with e_b the result's own score error;
+    with accurate scores it stays at the 1e-6 floor - two rows 2e-6 apart may not swap -
+    and a result whose scores are 1e-5 off widens it only to the 1e-5 cap."""
+    s = np.array([[0.2, 0.199998, 0.199996, 0.1]])
+    assert check_topk([[1, 0, 2]], [[0.199998, 0.2, 0.199996]], s, 3) != []
+    assert check_topk([[0, 1, 2]], [[0.2, 0.199998, 0.199996]], s, 3) == []
+    s2 = np.array([[0.2, 0.199995, 0.19997, 0.1]])  # 5e-6 / 2.5e-5 apart
+    assert check_topk([[1, 0, 2]], [[0.199995 + 4e-6, 0.2 - 4e-6, 0.19997]], s2, 3) == []
+    assert check_topk([[0, 2, 1]], [[0.2 + 4e-6, 0.19997, 0.199995]], s2, 3) != []
+
+
 def test_flat_golden_fixture(golden):
     f = np.load(golden + "/flat_golden.npz")
     c = synth.corpus(int(f["n"]), int(f["dim"]), clustered=True)
