@@ -651,17 +651,20 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
         // kPop keys (compare-exchange insertion), then rounds of a wave max whose lowest
         // holder pops its head - ~450 VALU instead of 32 rounds of kPer ballots (~4k
         // instructions while the workgroup's other waves wait at the barrier).  Same T.
-        // With kcert > 0 the pops run on to the kcert-th largest (Tk) as well.
-        constexpr int kPop = 16;  // >= kTsRank and >= the screens' k (kScreenMaxK)
-        unsigned top[kPop];
+        // With kcert > 0 the pops run on to the kcert-th largest (Tk) and the kPop-th (the
+        // floor) as well.  Each lane keeps only its best kDepth keys: a lane holding more
+        // of the top kPop drops some, so a popped rank can only come out LOWER than the
+        // true one - a lower tau (more survivors), never an unsound certificate.
+        constexpr int kPop = 32, kDepth = 8;  // kPop >= kTsRank, kScreenMaxK
+        unsigned top[kDepth];
 #pragma unroll
-        for (int i = 0; i < kPop; ++i) top[i] = 0u;
+        for (int i = 0; i < kDepth; ++i) top[i] = 0u;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
           if (64 * j < (int)gridDim.x) {  // (uniform) lists past the grid hold key 0
             unsigned x = key[q][j];
 #pragma unroll
-            for (int i = 0; i < kPop; ++i) {
+            for (int i = 0; i < kDepth; ++i) {
               const unsigned hi = max(top[i], x);
               x = min(top[i], x);
               top[i] = hi;
@@ -678,8 +681,8 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
           const unsigned long long holders = __ballot(top[0] == m);
           if (r + 1 < pops && lane == (int)__builtin_ctzll(holders)) {
 #pragma unroll
-            for (int i = 0; i + 1 < kPop; ++i) top[i] = top[i + 1];
-            top[kPop - 1] = 0u;
+            for (int i = 0; i + 1 < kDepth; ++i) top[i] = top[i + 1];
+            top[kDepth - 1] = 0u;
           }
         }
         if (kcert > 0 && stats) {
@@ -702,10 +705,12 @@ __global__ __launch_bounds__(256, kI8WgPerCu) void i8_thresh_kernel(
           const float tk = Tk == 0u ? -INFINITY : key_ord(Tk);
           const float tc = tk - 2.02f * Eb - 1e-6f;
           const float t8 = T == 0u ? -INFINITY : key_ord(T);
-          // ... floored at the kPop-th largest maximum (>= 16 sampled rows: ~256 survivors
+          // ... floored at the kPop-th largest maximum (>= 32 sampled rows: ~512 survivors
           // expected), so a k-th best sample far below the true k-th best (k large against
           // the query's cluster) cannot flood the survivor lists; then the certificate is
-          // no longer guaranteed, only likely
+          // no longer guaranteed, only likely.  (The 16th failed 7 of 100 clustered k = 5
+          // queries by < 0.001: their 16th sample was still a cluster-mate,
+          // tools/i8_cert_probe.py)
           const float tf = Tf == 0u ? -INFINITY : key_ord(Tf);
           const float t = fminf(t8, fmaxf(tc, tf));
           T = (MQ_I8_CERT_DBG & 2) ? T : t == -INFINITY ? 0u : ord_key(t);

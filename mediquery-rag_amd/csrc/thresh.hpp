@@ -63,7 +63,7 @@ struct ThreshI8Args {
   int* zero;                  // optional int the sample pass sets to 0 (the caller's fail count)
   // the certificate's tau (index.hip i8_finish_kernel): with the shadow's maxima `stats`
   // and the query's k, tau = min(the kTsRank-th largest sample list maximum, max(the k-th
-  // largest - 2E, the 16th largest)), E the screen's bound - tau + E < e_k then holds by
+  // largest - 2E, the 32nd largest)), E the screen's bound - tau + E < e_k then holds by
   // construction unless the floor applies
   const unsigned* stats = nullptr;
   int k = 0;                  // 0: tau = the kTsRank-th largest maximum only
