@@ -1031,8 +1031,11 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ src, 
 // rescaling order differs from one wave walking every tile, results agree to rounding).
 constexpr int kDh = 64;
 
-template <int NS>
-__global__ __launch_bounds__(64 * NS, NS == 1 ? 3 : 1) void attention_kernel(const float* __restrict__ qkv,
+// HB > 1 (NS = 1): one workgroup per (sequence, query tile) with one wave per head, so a
+// sequence's Q / K / V rows are read by waves issued together, whole 9 KB rows at a time
+// (one wave per workgroup read 256-B head slices of rows 9 KB apart, ~4 TB/s).
+template <int NS, int HB = 1>
+__global__ __launch_bounds__(64 * NS * HB, NS == 1 && HB == 1 ? 3 : 1) void attention_kernel(const float* __restrict__ qkv,
                                                             const int* __restrict__ mask, int L,
                                                             int H, int heads, int q_tiles,
                                                             float scale, float* __restrict__ ctx) {
@@ -1040,14 +1043,17 @@ __global__ __launch_bounds__(64 * NS, NS == 1 ? 3 : 1) void attention_kernel(con
   // [32][68] rows for staging (a 16-lane ds_read_b128 group hits 16 distinct bank groups),
   // [32][65] for the output
   constexpr int kSt = kDh + 4;
-  __shared__ __attribute__((aligned(16))) float tiles[NS][32 * kSt];
+  static_assert(HB == 1 || NS == 1, "heads per block or key splits");
+  __shared__ __attribute__((aligned(16))) float tiles[NS * HB][32 * kSt];
   __shared__ float wmax[NS > 1 ? NS : 1][32], wsum[NS > 1 ? NS : 1][32];
   const int wv = NS > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  float* tile = tiles[wv];
+  const int hw = HB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  float* tile = tiles[NS > 1 ? wv : hw];
   float(*obuf)[kDh + 1] = reinterpret_cast<float(*)[kDh + 1]>(tile);
   const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int qt = blockIdx.x % q_tiles, h = (blockIdx.x / q_tiles) % heads;
-  const int bseq = blockIdx.x / (q_tiles * heads);
+  const int hgroups = heads / HB;
+  const int qt = blockIdx.x % q_tiles, h = ((blockIdx.x / q_tiles) % hgroups) * HB + hw;
+  const int bseq = blockIdx.x / (q_tiles * hgroups);
   const int q0 = qt * 32;
   const int64_t row0 = (int64_t)bseq * L;
   const int ld = 3 * H;
@@ -1177,7 +1183,10 @@ void launch_attention(int B, int L, int heads, int qt, int H, float scale, const
                       const int* mask, float* ctx, hipStream_t s) {
   const int triples = B * heads * qt, key_tiles = (L + 31) / 32;
   const dim3 grid(triples);
-  if (key_tiles >= 8 && triples <= 256)
+  if (key_tiles == 1 && heads == 12 && triples >= 12 * 256)  // BERT-base batches: 12 heads per workgroup
+    hipLaunchKernelGGL((attention_kernel<1, 12>), dim3(B * qt), dim3(768), 0, s, qkv, mask, L, H, heads, qt, scale,
+                       ctx);
+  else if (key_tiles >= 8 && triples <= 256)
     hipLaunchKernelGGL(attention_kernel<8>, grid, dim3(512), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
   else if (key_tiles >= 4 && triples <= 512)
     hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(256), 0, s, qkv, mask, L, H, heads, qt, scale, ctx);
