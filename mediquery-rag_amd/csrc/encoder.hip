@@ -1721,6 +1721,11 @@ void launch_gemm(const GemmArgs& g, int num_cus, hipStream_t s, bool x6 = false,
     launch_splitk<EPI>(g, S, s);
     return;
   }
+  // split-f32 pays where its tiles fill the chip; a GEMM of fewer rows (a long single
+  // query: M = 512 is 48 K2p tiles on 256 CUs) runs the exact-f32 tiles instead - narrower
+  // tiles spread further, and exact f32 is at least as accurate (L = 512 single query:
+  // 3.09-3.16 ms p50 on either split-f32 path, 2.45 on exact f32)
+  if (x6 && (int64_t)((g.M + 127) / 128) * ((g.N + 191) / 192) < num_cus) x6 = false;
   if (x6 && g.W3) {  // split-f32 on the pre-split weights (K2p)
     launch_gemm_x6p(X6pArgs{g.A, g.lda, g.W3, g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K}, EPI, -1, num_cus,
                     s);

@@ -286,9 +286,9 @@ def test_resident_layers_changes_only_the_cache_policy(require_gpu):
 
 @pytest.mark.parametrize("B,L,layers,pool", [
     (256, 32, 12, None),           # the bench shape: every batched GEMM on K2p
-    (9, 33, 3, POOL_MEAN),         # 297 rows: ragged 128-row tiles
-    (9, 33, 3, None),              # CLS-only last layer: K/V rows of the W3 image
-    (300, 3, 2, None),             # many short sequences
+    (9, 33, 3, POOL_MEAN),         # 297 rows: under-fills the chip -> exact-f32 tiles in both modes
+    (9, 33, 3, None),              # CLS-only last layer (K2p tiles are covered shape by shape
+    (300, 3, 2, None),             # in test_gpu_gemm_x6p.py, ragged M / N included)
 ])
 def test_x6_presplit_bit_identical(require_gpu, B, L, layers, pool):
     """Split-f32 precision: the batched GEMMs on the pre-split W3 weights (K2p, default)
