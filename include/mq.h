@@ -45,7 +45,9 @@ extern "C" {
 #define MQ_DTYPE_F32 0    /* exact fp32 MFMA (v_mfma_f32_32x32x2_f32)                     */
 #define MQ_DTYPE_BF16 1   /* bf16 storage (coarse paths)                                    */
 #define MQ_DTYPE_F32X6 2  /* fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMAs per
-                           * product, fp32 accumulate: fp32-class error, 2.67x the MFMA rate */
+                           * product, fp32 accumulate: fp32-class error, 2.67x the MFMA rate;
+                           * encoder GEMMs too small to fill the chip (few-row / long single
+                           * queries) run exact fp32, which is faster there */
 #define MQ_DTYPE_F32_SCREEN 3 /* search only: exact fp32 top-k through certified screens -
                                * bf16 shadow scan for k + 8..16 candidates, fp32 re-rank,
                                * proven error bound; uncertified queries re-run on the
