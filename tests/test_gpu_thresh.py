@@ -181,3 +181,22 @@ def test_config5_full_size_recall(require_gpu):
     normed = torch.nn.functional.normalize(rows, dim=1)
     dots = (normed[i] * q[:, None, :]).sum(-1)  # fp32 dots of the returned rows
     assert float((dots - s).abs().max()) < 1e-5
+    # against float64 (the full-size case compared only with the HIP exact
+    # path): the exact path within tie groups, with its tie swaps counted, and the bf16
+    # path's recall@50
+    del normed
+    normed64 = torch.nn.functional.normalize(rows.double(), dim=1)
+    ref_full = q.double() @ normed64.T
+    del normed64
+    rv, ri = torch.topk(ref_full, k + 1, dim=1)
+    fails = check_topk(exact, s2.cpu().numpy(), None, k, ref_top=(rv.cpu().numpy(), ri.cpu().numpy()),
+                       n_rows=1_000_000,
+                       ref_lookup=lambda b, ids: ref_full[b, torch.as_tensor(ids, device=dev)].cpu().numpy())
+    assert fails == [], fails[:3]
+    swaps = int((i2 != ri[:, :k]).sum())  # positions inside a tie group that differ from float64
+    ref_ids = ri[:, :k].cpu().numpy()
+    hits64 = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(got, ref_ids))
+    print("config5: exact-path tie swaps vs float64 %d of %d, bf16 recall@50 vs float64 %.5f"
+          % (swaps, 256 * k, hits64 / (256 * k)))
+    assert swaps <= 256 * k // 500, swaps
+    assert hits64 / (256 * k) >= 0.98, hits64 / (256 * k)
