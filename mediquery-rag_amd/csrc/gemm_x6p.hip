@@ -119,7 +119,10 @@ struct X6pTile {
   // registers - at KS = 1 that happens one iteration early (the fragments run one k-step
   // ahead), so the ring can run one stage further ahead
   static constexpr int AHEAD = KS == 1 ? NBUF : NBUF - 1;
-  static constexpr int GM = 4;  // row tiles per band of the tile walk
+#ifndef MQ_X6P_GM  // tuning default: 8 row tiles per band (half the W3 column blocks per XCD
+#define MQ_X6P_GM 4  // round) measured the same at every headline shape (tools/gpu_ab_x6p.sh)
+#endif
+  static constexpr int GM = MQ_X6P_GM;  // row tiles per band of the tile walk
   static_assert(LDR ? NW == 4 : NW == 8, "8-wave workgroups");
   static_assert(!SCHED || (CNT_HI - 1) * DSTEP < TM * TN * 6, "DMAs per k-step slots");
   static_assert(AHEAD >= 2 && NBUF * STAGE <= 160 * 1024, "LDS ring");
