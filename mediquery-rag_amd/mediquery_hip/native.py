@@ -300,6 +300,14 @@ def mask_eval(codes, lut, bits, mode, stream=None):
               mode, _lib.stream_handle(stream))
 
 
+def mask_eval64(codes, lut, bits, mode, stream=None):
+    """mask_eval with a table of <= 64 entries passed by value (numpy bool / uint8 lut)."""
+    lut = np.asarray(lut).astype(bool)
+    word = sum(1 << i for i in np.flatnonzero(lut).tolist())
+    _lib.call("mq_mask_eval64", _lib.ptr(codes), codes.numel(), ctypes.c_uint64(word), len(lut), _lib.ptr(bits),
+              mode, _lib.stream_handle(stream))
+
+
 def mask_combine(dst, src, mode, stream=None):
     """dst (mode)= src (None: all ones; MQ_MASK_CLEAR: zeros) on the device."""
     _lib.call("mq_mask_combine", _lib.ptr(dst), _lib.ptr(src), dst.numel(), mode, _lib.stream_handle(stream))

@@ -42,7 +42,7 @@ import numpy as np
 
 from . import _lib
 from .compat import Document, VectorStoreBase
-from .native import FlatIndex, mask_combine, mask_eval
+from .native import FlatIndex, mask_combine, mask_eval, mask_eval64
 
 DEFAULT_K = 4  # LangChain VectorStore.similarity_search default; the reference passes k=5
 
@@ -202,8 +202,11 @@ class _MetaColumns:
                         if not _pred(op, None, x):
                             mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
                         continue
-                    lut = torch.from_numpy(self._lut(col[1], op, x)).to(dev)
-                    mask_eval(self.dev_codes(key, dev), lut, bits, _lib.MQ_MASK_AND)
+                    lut = self._lut(col[1], op, x)
+                    if len(lut) <= 64:  # by value: no host-to-device copy
+                        mask_eval64(self.dev_codes(key, dev), lut, bits, _lib.MQ_MASK_AND)
+                    else:
+                        mask_eval(self.dev_codes(key, dev), torch.from_numpy(lut).to(dev), bits, _lib.MQ_MASK_AND)
 
     def mask(self, where):
         out = np.ones(self.n, bool)
@@ -483,12 +486,9 @@ class HipChroma(VectorStoreBase):
         keepm[drop] = False
         keep = np.flatnonzero(keepm)
         self._index.select(keep, out=self._index)  # device compaction, rows bit-identical
-        n = len(self._ids)
+        keepl = keepm.tolist()
         for name in ("_ids", "_texts", "_metas"):
-            arr = np.empty(n, object)
-            for r, v in enumerate(getattr(self, name)):  # (dicts must not be unpacked)
-                arr[r] = v
-            setattr(self, name, arr[keep].tolist())
+            setattr(self, name, [v for v, kp in zip(getattr(self, name), keepl) if kp])
         self._cols.compact(keep)
         self._id_row = {i: r for r, i in enumerate(self._ids)}
         self._version += 1
@@ -547,16 +547,25 @@ class HipChroma(VectorStoreBase):
         """(Document, cosine similarity) pairs - the index's native score."""
         return [(self._doc(r), c) for r, c in self._search_rows(self._embed_query(query), k, filter)]
 
-    def similarity_search_batch(self, queries, k=DEFAULT_K):
-        """Many queries in one encoder batch + one device search (the throughput path)."""
+    def similarity_search_batch(self, queries, k=DEFAULT_K, filter=None):
+        """Many queries in one encoder batch + one device search (the throughput path).
+        With `filter`, the where-mask is built once on the device and every query runs
+        the masked search over it."""
         n = 0 if self._index is None else len(self._index)
         if n == 0 or not queries or k <= 0:
             return [[] for _ in queries]
-        kk = _check_k(k, n)
         if hasattr(self._embedding_function, "embed_array"):
             q = self._embedding_function.embed_array(list(queries))
         else:
             q = np.asarray(self._embedding_function.embed_documents(list(queries)), np.float32)
+        if filter:
+            kk = k if k <= _lib.MQ_MAX_K else _check_k(k, int(self._cols.mask(filter).sum()))
+            if kk == 0:
+                return [[] for _ in queries]
+            bits = self._cols.dmask(filter, self._device)
+            rows = [self._index.search_masked(qv, int(kk), bits)[1][0] for qv in q]
+            return [[self._doc(int(r)) for r in row if r >= 0] for row in rows]
+        kk = _check_k(k, n)
         _, ids = self._index.search(q, kk)
         return [[self._doc(int(r)) for r in row if r >= 0] for row in ids]
 

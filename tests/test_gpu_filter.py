@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from mediquery_hip import _lib, synth
-from mediquery_hip.native import FlatIndex, mask_combine, mask_eval
+from mediquery_hip.native import FlatIndex, mask_combine, mask_eval, mask_eval64
 from mediquery_hip.vectorstore import HipChroma, _match
 from oracle.flat import check_topk
 
@@ -60,6 +60,13 @@ def test_mask_kernels_match_numpy(require_gpu):
         assert np.array_equal(got, want | want2), n
         mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
         assert int(bits.abs().sum()) == 0
+        # the by-value table (<= 64 entries) gives the same words
+        mask_combine(bits, None, _lib.MQ_MASK_SET)
+        mask_eval64(dc, lut, bits, _lib.MQ_MASK_AND)
+        mask_eval(dc, torch.as_tensor(lut2, device=dev), tmp, _lib.MQ_MASK_SET)
+        mask_combine(bits, tmp, _lib.MQ_MASK_OR)
+        got = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(got, want | want2), n
 
 
 @pytest.fixture(scope="module")
@@ -107,3 +114,27 @@ def test_wide_filters_certify_on_the_int8_screen(big_store):
         q = rows64[int(rng.integers(0, len(metas)))].float().cpu().numpy()
         store._search_rows(q, 5, {"src": j % 7})
     assert store._index.masked_gathers - g0 <= 2
+
+
+def test_batch_search_with_filter_matches_single(require_gpu, big_store):
+    """similarity_search_batch(filter=) (one device mask, one masked search per query)
+    returns what the single-query path returns, query by query."""
+    store, rows64, metas = big_store
+
+    class _Emb:  # the batch path embeds through the store's function: vectors pass through
+        def __init__(self, vecs):
+            self.vecs = vecs
+
+        def embed_documents(self, texts):
+            return [self.vecs[int(t)] for t in texts]
+
+    rng = np.random.default_rng(21)
+    vecs = [rows64[int(rng.integers(0, len(metas)))].float().cpu().numpy() for _ in range(6)]
+    store._embedding_function = _Emb(vecs)
+    where = {"$or": [{"src": 2}, {"year": {"$lt": 5}}]}
+    got = store.similarity_search_batch([str(j) for j in range(6)], k=5, filter=where)
+    for j, docs in enumerate(got):
+        want = [r for r, _ in store._search_rows(vecs[j], 5, where)]
+        assert [int(d.id[2:]) for d in docs] == want
+    store._embedding_function = None
+
