@@ -172,10 +172,11 @@ int mq_index_read_timing(mq_index* ix, float* ms, int n);
 #define MQ_MASK_CLEAR 3
 int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut, uint32_t* bits, int mode,
                  void* stream);
-/* mq_mask_eval with the table passed by value: bit i of lut_bits = lut[i], n_lut <= 64 (a
- * key with few distinct values: no host-to-device copy per condition). */
-int mq_mask_eval64(const int32_t* codes, int64_t n, uint64_t lut_bits, int n_lut, uint32_t* bits, int mode,
-                   void* stream);
+/* mq_mask_eval with the table passed by value: lut_words a HOST array of ceil(n_lut / 64)
+ * words, bit i % 64 of word i / 64 = lut[i], n_lut <= 256 (a key with few distinct values:
+ * no host-to-device copy per condition). */
+int mq_mask_eval_bits(const int32_t* codes, int64_t n, const uint64_t* lut_words, int n_lut, uint32_t* bits,
+                      int mode, void* stream);
 int mq_mask_combine(uint32_t* dst, const uint32_t* src, int64_t n_words, int mode, void* stream);
 /* Exact top-k of one query over the allowed rows (same ranking and padding as
  * mq_index_search; bits: a device mask of >= ceil(n / 32) words).  The int8 certified

@@ -63,17 +63,21 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 // A metadata condition over one column: codes[r] (-1 = key absent in row r) index a
 // per-distinct-value truth table lut (its last entry: absent); 64 rows per wave, one
 // ballot, lanes 0 / 32 write the two words.  mode: MQ_MASK_SET / AND / OR into bits.
-// (lut == NULL: the table is the bits of lut64, n_lut <= 64 - no host-to-device copy for it)
+// (lut == NULL: the table is the bits of lw, n_lut <= 256 - passed by value, no
+// host-to-device copy for it)
+struct LutWords {
+  unsigned long long w[4];
+};
 __global__ __launch_bounds__(256) void mask_eval_kernel(const int* __restrict__ codes, int64_t n,
-                                                        const unsigned char* __restrict__ lut,
-                                                        unsigned long long lut64, int n_lut,
-                                                        unsigned* __restrict__ bits, int mode) {
+                                                        const unsigned char* __restrict__ lut, LutWords lw,
+                                                        int n_lut, unsigned* __restrict__ bits, int mode) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   bool v = false;
   if (r < n) {
     const int c = codes[r];
     const int i = (c >= 0 && c < n_lut - 1) ? c : n_lut - 1;
-    v = lut ? lut[i] != 0 : ((lut64 >> i) & 1ull) != 0;
+    const unsigned long long w = i < 64 ? lw.w[0] : i < 128 ? lw.w[1] : i < 192 ? lw.w[2] : lw.w[3];
+    v = lut ? lut[i] != 0 : ((w >> (i & 63)) & 1ull) != 0;
   }
   const unsigned long long b = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -2372,21 +2376,23 @@ int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut,
   if (n == 0) return MQ_OK;
   MQ_CHECK_ARG(codes && lut && bits, "NULL buffer");
   hipLaunchKernelGGL(mask_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const int*)codes, n, (const unsigned char*)lut, 0ull, n_lut, (unsigned*)bits, mode);
+                     (const int*)codes, n, (const unsigned char*)lut, LutWords{}, n_lut, (unsigned*)bits, mode);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
 
-int mq_mask_eval64(const int32_t* codes, int64_t n, uint64_t lut_bits, int n_lut, uint32_t* bits, int mode,
-                   void* stream) {
+int mq_mask_eval_bits(const int32_t* codes, int64_t n, const uint64_t* lut_words, int n_lut, uint32_t* bits,
+                      int mode, void* stream) {
   clear_error();
-  MQ_CHECK_ARG(n >= 0 && n_lut >= 1 && n_lut <= 64, "n_lut must be in [1, 64]");
+  MQ_CHECK_ARG(n >= 0 && n_lut >= 1 && n_lut <= 256, "n_lut must be in [1, 256]");
   MQ_CHECK_ARG(mode == MQ_MASK_SET || mode == MQ_MASK_AND || mode == MQ_MASK_OR, "bad mask mode %d", mode);
+  MQ_CHECK_ARG(lut_words, "NULL table");
   if (n == 0) return MQ_OK;
   MQ_CHECK_ARG(codes && bits, "NULL buffer");
+  LutWords lw{};
+  for (int i = 0; i < (n_lut + 63) / 64; ++i) lw.w[i] = lut_words[i];
   hipLaunchKernelGGL(mask_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const int*)codes, n, (const unsigned char*)nullptr, (unsigned long long)lut_bits, n_lut,
-                     (unsigned*)bits, mode);
+                     (const int*)codes, n, (const unsigned char*)nullptr, lw, n_lut, (unsigned*)bits, mode);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }

@@ -83,7 +83,7 @@ SIGNATURES = {
     "mq_index_save_rows": (_I, [_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
     "mq_index_load_append": (_I, [_P, ctypes.c_char_p]),
     "mq_mask_eval": (_I, [_P, _I64, _P, _I, _P, _I, _P]),
-    "mq_mask_eval64": (_I, [_P, _I64, ctypes.c_uint64, _I, _P, _I, _P]),
+    "mq_mask_eval_bits": (_I, [_P, _I64, _P, _I, _P, _I, _P]),
     "mq_mask_combine": (_I, [_P, _P, _I64, _I, _P]),
     "mq_index_search_masked": (_I, [_P, _P, _I, _P, _P, _P, _I, _P]),
     "mq_index_masked_gathers": (_I, [_P, ctypes.POINTER(_I64)]),

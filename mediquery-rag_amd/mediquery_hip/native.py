@@ -300,11 +300,13 @@ def mask_eval(codes, lut, bits, mode, stream=None):
               mode, _lib.stream_handle(stream))
 
 
-def mask_eval64(codes, lut, bits, mode, stream=None):
-    """mask_eval with a table of <= 64 entries passed by value (numpy bool / uint8 lut)."""
+def mask_eval_bits(codes, lut, bits, mode, stream=None):
+    """mask_eval with a table of <= 256 entries passed by value (numpy bool / uint8 lut)."""
     lut = np.asarray(lut).astype(bool)
-    word = sum(1 << i for i in np.flatnonzero(lut).tolist())
-    _lib.call("mq_mask_eval64", _lib.ptr(codes), codes.numel(), ctypes.c_uint64(word), len(lut), _lib.ptr(bits),
+    words = np.zeros(4, dtype=np.uint64)
+    for i in np.flatnonzero(lut).tolist():
+        words[i >> 6] |= np.uint64(1 << (i & 63))
+    _lib.call("mq_mask_eval_bits", _lib.ptr(codes), codes.numel(), _lib.ptr(words), len(lut), _lib.ptr(bits),
               mode, _lib.stream_handle(stream))
 
 

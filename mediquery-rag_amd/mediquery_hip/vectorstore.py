@@ -42,7 +42,7 @@ import numpy as np
 
 from . import _lib
 from .compat import Document, VectorStoreBase
-from .native import FlatIndex, mask_combine, mask_eval, mask_eval64
+from .native import FlatIndex, mask_combine, mask_eval, mask_eval_bits
 
 DEFAULT_K = 4  # LangChain VectorStore.similarity_search default; the reference passes k=5
 
@@ -116,6 +116,7 @@ class _MetaColumns:
         self.cols = {}  # key -> [codes np.int32 (capacity >= n), values list, {hash key: code}]
         self.ver = 0    # bumped by append / compact (device mirrors are per version)
         self.dev = {}   # key -> (ver, device int32 codes [n])
+        self._num_cache = {}  # id(values list) -> (len, float64 array or None: not all numeric)
 
     @staticmethod
     def _hkey(v):
@@ -154,11 +155,29 @@ class _MetaColumns:
         self.n = len(keep)
         self.ver += 1
 
+    _NUM_OPS = {"$eq": np.equal, "$ne": np.not_equal, "$gt": np.greater, "$gte": np.greater_equal,
+                "$lt": np.less, "$lte": np.less_equal}
+
     @staticmethod
-    def _lut(values, op, x):
-        """Truth table of one condition over a column's distinct values (+ absent, last)."""
+    def _is_num(v):  # a number float64 holds exactly (ints past 2^53 take the exact path)
+        return (isinstance(v, float) or (isinstance(v, int) and abs(v) < 2 ** 53)) and not isinstance(v, bool)
+
+    def _lut(self, values, op, x):
+        """Truth table of one condition over a column's distinct values (+ absent, last).
+        A comparison of a number against an all-numeric column is one numpy op (the
+        per-value Python predicate cost ~0.4 us a value); anything else goes value by value
+        through _pred (Chroma's typed comparison: mixed types never match)."""
         lut = np.zeros(len(values) + 1, np.uint8)
         lut[-1] = _pred(op, None, x)
+        if op in self._NUM_OPS and self._is_num(x) and len(values) > 8:
+            nums = self._num_cache.get(id(values))
+            if nums is None or nums[0] != len(values):
+                ok = all(self._is_num(v) for v in values)
+                nums = (len(values), np.array(values, dtype=np.float64) if ok else None)
+                self._num_cache[id(values)] = nums
+            if nums[1] is not None:
+                lut[:-1] = self._NUM_OPS[op](nums[1], float(x))
+                return lut
         for cv, v in enumerate(values):
             lut[cv] = _pred(op, v, x)
         return lut
@@ -203,8 +222,8 @@ class _MetaColumns:
                             mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
                         continue
                     lut = self._lut(col[1], op, x)
-                    if len(lut) <= 64:  # by value: no host-to-device copy
-                        mask_eval64(self.dev_codes(key, dev), lut, bits, _lib.MQ_MASK_AND)
+                    if len(lut) <= 256:  # by value: no host-to-device copy
+                        mask_eval_bits(self.dev_codes(key, dev), lut, bits, _lib.MQ_MASK_AND)
                     else:
                         mask_eval(self.dev_codes(key, dev), torch.from_numpy(lut).to(dev), bits, _lib.MQ_MASK_AND)
 

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from mediquery_hip import _lib, synth
-from mediquery_hip.native import FlatIndex, mask_combine, mask_eval, mask_eval64
+from mediquery_hip.native import FlatIndex, mask_combine, mask_eval, mask_eval_bits
 from mediquery_hip.vectorstore import HipChroma, _match
 from oracle.flat import check_topk
 
@@ -60,9 +60,9 @@ def test_mask_kernels_match_numpy(require_gpu):
         assert np.array_equal(got, want | want2), n
         mask_combine(bits, None, _lib.MQ_MASK_CLEAR)
         assert int(bits.abs().sum()) == 0
-        # the by-value table (<= 64 entries) gives the same words
+        # the by-value table (<= 256 entries) gives the same words
         mask_combine(bits, None, _lib.MQ_MASK_SET)
-        mask_eval64(dc, lut, bits, _lib.MQ_MASK_AND)
+        mask_eval_bits(dc, lut, bits, _lib.MQ_MASK_AND)
         mask_eval(dc, torch.as_tensor(lut2, device=dev), tmp, _lib.MQ_MASK_SET)
         mask_combine(bits, tmp, _lib.MQ_MASK_OR)
         got = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
@@ -137,4 +137,21 @@ def test_batch_search_with_filter_matches_single(require_gpu, big_store):
         want = [r for r, _ in store._search_rows(vecs[j], 5, where)]
         assert [int(d.id[2:]) for d in docs] == want
     store._embedding_function = None
+
+
+def test_mask_by_value_table_past_64_entries(require_gpu):
+    """Tables of 65..256 entries (keys with that many distinct values) by value: the words
+    past the first select the right bits."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(9)
+    for n_lut in (65, 130, 200, 256):
+        n = 5000
+        codes = rng.integers(-1, n_lut - 1, n).astype(np.int32)
+        lut = rng.integers(0, 2, n_lut).astype(np.uint8)
+        want = lut[np.where(codes >= 0, codes, n_lut - 1)].astype(bool)
+        bits = torch.empty((n + 31) // 32, dtype=torch.int32, device=dev)
+        mask_eval_bits(torch.as_tensor(codes, device=dev), lut, bits, _lib.MQ_MASK_SET)
+        got = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert np.array_equal(got, want), n_lut
 
