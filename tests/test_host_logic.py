@@ -143,6 +143,25 @@ def test_metadata_mixed_types_compare_as_no_match():
     assert [_match(m, {"n": {"$gt": "5"}}) for m in metas] == [False, True, False, False, False]
 
 
+def test_metadata_numeric_tables_equal_row_filter():
+    """The numpy truth tables of numeric comparisons (columns of > 8 distinct numbers)
+    equal the row-wise semantics: ints and floats mixed, a bool among ints (exact path),
+    an int past 2^53 (exact path), NaN."""
+    from mediquery_hip.vectorstore import _MetaColumns
+    metas = [{"n": i % 100, "f": (i % 37) / 3.0} for i in range(2000)]
+    metas[3]["n"] = 2.5
+    metas[7]["f"] = float("nan")
+    metas2 = [dict(m) for m in metas]
+    metas2[11]["n"] = True
+    metas2[12]["f"] = 2 ** 60 + 1
+    for ms in (metas, metas2):
+        cols = _MetaColumns()
+        cols.append(ms)
+        for w in ({"n": {"$lt": 50}}, {"n": {"$gte": 2.5}}, {"n": {"$eq": 1}}, {"n": {"$ne": 4}},
+                  {"f": {"$gt": 3.5}}, {"f": {"$lte": 2 ** 60}}, {"n": {"$gt": True}}):
+            np.testing.assert_array_equal(cols.mask(w), [_match(m, w) for m in ms], err_msg=str(w))
+
+
 def test_orphan_slab_sweep_spares_sibling_collections_and_writes_in_flight(tmp_path):
     """persist()'s sweep deletes only THIS collection's slabs that this instance replaced
     or that are stale crash leftovers: never a sibling collection's ('docs' vs 'docs.v2'),
