@@ -47,6 +47,33 @@ struct Status {
     if (!(cond)) MQ_FAIL(MQ_EINVAL, __VA_ARGS__); \
   } while (0)
 
+// Grow-only pinned host staging for the host-pointer entry points: a pageable 3-KB copy
+// is staged by the runtime and synchronous (~10-20 us each way on the single-query path);
+// from pinned memory it is one DMA on the stream.
+struct PinBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return MQ_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess)
+      MQ_FAIL(MQ_ENOMEM, "hipHostMalloc(%zu bytes) failed", need);
+    bytes = need;
+    return MQ_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
 // Run `fn` with `device` current, restoring the caller's device afterwards.
 struct DeviceGuard {
   int prev = -1;

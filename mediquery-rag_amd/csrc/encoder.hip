@@ -1796,6 +1796,7 @@ enum Stage { ST_EMBED = 0, ST_QKV, ST_ATTN, ST_OPROJ, ST_LN, ST_FFN_UP, ST_FFN_D
 
 struct mq_encoder {
   int device = 0;
+  PinBuf pin;  // pinned staging of the host-pointer embed path (few tokens)
   mq_bert_config cfg{};
   int precision = MQ_DTYPE_F32;
   bool loaded = false;
@@ -2396,6 +2397,7 @@ int mq_encoder_destroy(mq_encoder* e) {
       b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
+    e->pin.release();
     for (auto& g : e->graphs) (void)hipGraphExecDestroy(g.exec);
     if (e->cap_stream) (void)hipStreamDestroy(e->cap_stream);
   }
@@ -2647,8 +2649,18 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
     rc = e->io_out.ensure((size_t)B * c.hidden);
     if (rc) return rc;
     const hipMemcpyKind kind = io_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    MQ_HIP(hipMemcpyAsync(e->io_ids, ids, M * 4, kind, s));
-    MQ_HIP(hipMemcpyAsync(e->io_mask, mask, M * 4, kind, s));
+    if (!io_on_device && M * 8 + (size_t)B * c.hidden * 4 <= (1u << 20)) {
+      // few tokens (single queries): ids and mask through pinned staging, one DMA each
+      rc = e->pin.ensure(M * 8 + (size_t)B * c.hidden * 4);
+      if (rc) return rc;
+      memcpy(e->pin.as<unsigned char>(), ids, M * 4);
+      memcpy(e->pin.as<unsigned char>() + M * 4, mask, M * 4);
+      MQ_HIP(hipMemcpyAsync(e->io_ids, e->pin.p, M * 4, kind, s));
+      MQ_HIP(hipMemcpyAsync(e->io_mask, e->pin.as<unsigned char>() + M * 4, M * 4, kind, s));
+    } else {
+      MQ_HIP(hipMemcpyAsync(e->io_ids, ids, M * 4, kind, s));
+      MQ_HIP(hipMemcpyAsync(e->io_mask, mask, M * 4, kind, s));
+    }
     dids = e->io_ids;
     dmask = e->io_mask;
     dout = e->io_out.p;
@@ -2662,8 +2674,16 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   if (io_on_device && dout != out)
     MQ_HIP(hipMemcpyAsync(out, dout, (size_t)B * c.hidden * 4, hipMemcpyDeviceToDevice, s));
   if (!io_on_device) {
-    MQ_HIP(hipMemcpyAsync(out, dout, (size_t)B * c.hidden * 4, hipMemcpyDeviceToHost, s));
-    MQ_HIP(hipStreamSynchronize(s));
+    const size_t ob = (size_t)B * c.hidden * 4;
+    if (M * 8 + ob <= (1u << 20)) {  // (the pinned staging above)
+      unsigned char* hp = e->pin.as<unsigned char>() + M * 8;
+      MQ_HIP(hipMemcpyAsync(hp, dout, ob, hipMemcpyDeviceToHost, s));
+      MQ_HIP(hipStreamSynchronize(s));
+      memcpy(out, hp, ob);
+    } else {
+      MQ_HIP(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, s));
+      MQ_HIP(hipStreamSynchronize(s));
+    }
   }
   return MQ_OK;
 }

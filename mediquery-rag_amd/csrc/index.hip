@@ -1365,6 +1365,7 @@ struct mq_index {
   DevBuf i8c_cs, i8c_ci, i8c_count;  // K9q survivors compacted (the debug select path)
   DevBuf msel, mblk;     // masked search: the allowed rows (sorted) + per-block counts
   DevBuf mres_s, mres_i;  // masked search: results staged for the host
+  PinBuf pin;             // pinned host staging of the host-pointer search calls
   mq_index* msub = nullptr;  // masked search fallback: the allowed rows gathered
   DevBuf rows8, scale8, err8, stats8;  // int8 shadow [cap, dim] + per-row scales, errors ||c - scale r8|| + maxima (as stats16)
   int64_t n8 = 0;                // rows already mirrored into rows8
@@ -2148,6 +2149,7 @@ int mq_index_destroy(mq_index* ix) {
     DeviceGuard dg(ix->device);
     if (ix->rows) (void)hipFree(ix->rows);
     if (ix->host_flag) (void)hipHostFree(ix->host_flag);
+    ix->pin.release();
     ix->stage.release();
     ix->cand_s.release();
     ix->cand_i.release();
@@ -2424,17 +2426,23 @@ int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32
     MQ_HIP(hipStreamSynchronize(s));
     return MQ_OK;
   }
-  int rc = ix->stage.ensure((size_t)ix->dim * 4);
-  if (!rc) rc = ix->mres_s.ensure((size_t)k * 4);
-  if (!rc) rc = ix->mres_i.ensure((size_t)k * 8);
+  const size_t qb = (size_t)ix->dim * 4, sb = (size_t)k * 4, ib = (size_t)k * 8;
+  int rc = ix->stage.ensure(qb);
+  if (!rc) rc = ix->mres_s.ensure(sb);
+  if (!rc) rc = ix->mres_i.ensure(ib);
+  if (!rc) rc = ix->pin.ensure(qb + sb + ib);  // pinned staging (see mq_index_search)
   if (rc) return rc;
-  MQ_HIP(hipMemcpyAsync(ix->stage.p, query, (size_t)ix->dim * 4, hipMemcpyHostToDevice, s));
+  unsigned char* hp = ix->pin.as<unsigned char>();
+  memcpy(hp, query, qb);
+  MQ_HIP(hipMemcpyAsync(ix->stage.p, hp, qb, hipMemcpyHostToDevice, s));
   rc = search_masked(ix, ix->stage.as<float>(), k, (const unsigned*)bits, ix->mres_s.as<float>(),
                      ix->mres_i.as<int64_t>(), s);
   if (rc) return rc;
-  MQ_HIP(hipMemcpyAsync(out_scores, ix->mres_s.p, (size_t)k * 4, hipMemcpyDeviceToHost, s));
-  MQ_HIP(hipMemcpyAsync(out_ids, ix->mres_i.p, (size_t)k * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(hp + qb, ix->mres_s.p, sb, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(hp + qb + sb, ix->mres_i.p, ib, hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
+  memcpy(out_scores, hp + qb, sb);
+  memcpy(out_ids, hp + qb + sb, ib);
   return MQ_OK;
 }
 
@@ -2458,17 +2466,32 @@ int mq_index_search(mq_index* ix, const float* queries, int64_t nq, int k, float
   DeviceGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
   if (io_on_device) return search_device(ix, queries, nq, k, out_scores, out_ids, s);
-  int rc = ix->stage.ensure((size_t)nq * ix->dim * 4);
-  if (!rc) rc = ix->out_s.ensure((size_t)nq * k * 4);
-  if (!rc) rc = ix->out_i.ensure((size_t)nq * k * 8);
+  const size_t qb = (size_t)nq * ix->dim * 4, sb = (size_t)nq * k * 4, ib = (size_t)nq * k * 8;
+  int rc = ix->stage.ensure(qb);
+  if (!rc) rc = ix->out_s.ensure(sb);
+  if (!rc) rc = ix->out_i.ensure(ib);
+  // pinned staging for the few-query path (a batch's bytes go pageable: the copy dominates
+  // neither way, and the pinned buffer stays small)
+  const bool pin = qb <= (1u << 20);
+  if (!rc && pin) rc = ix->pin.ensure(qb + sb + ib);
   if (rc) return rc;
-  MQ_HIP(hipMemcpyAsync(ix->stage.p, queries, (size_t)nq * ix->dim * 4, hipMemcpyHostToDevice, s));
+  unsigned char* hp = ix->pin.as<unsigned char>();
+  if (pin) {
+    memcpy(hp, queries, qb);
+    MQ_HIP(hipMemcpyAsync(ix->stage.p, hp, qb, hipMemcpyHostToDevice, s));
+  } else {
+    MQ_HIP(hipMemcpyAsync(ix->stage.p, queries, qb, hipMemcpyHostToDevice, s));
+  }
   rc = search_device(ix, ix->stage.as<float>(), nq, k, ix->out_s.as<float>(),
                      ix->out_i.as<int64_t>(), s);
   if (rc) return rc;
-  MQ_HIP(hipMemcpyAsync(out_scores, ix->out_s.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
-  MQ_HIP(hipMemcpyAsync(out_ids, ix->out_i.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(pin ? (void*)(hp + qb) : (void*)out_scores, ix->out_s.p, sb, hipMemcpyDeviceToHost, s));
+  MQ_HIP(hipMemcpyAsync(pin ? (void*)(hp + qb + sb) : (void*)out_ids, ix->out_i.p, ib, hipMemcpyDeviceToHost, s));
   MQ_HIP(hipStreamSynchronize(s));
+  if (pin) {
+    memcpy(out_scores, hp + qb, sb);
+    memcpy(out_ids, hp + qb + sb, ib);
+  }
   return MQ_OK;
 }
 
