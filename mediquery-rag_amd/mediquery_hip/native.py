@@ -168,6 +168,9 @@ class FlatIndex:
         """Exact top-k of one query over the rows allowed by `bits` (a device mask tensor of
         >= ceil(n / 32) int32 words, bit r % 32 of word r / 32 = row r; mask_eval builds it)."""
         q = np.ascontiguousarray(query, dtype=np.float32).reshape(self.dim)
+        if not (getattr(bits, "is_cuda", False) and bits.element_size() == 4 and bits.is_contiguous()
+                and bits.numel() >= (len(self) + 31) // 32):
+            raise ValueError("bits must be a contiguous 32-bit device tensor of >= ceil(n / 32) words")
         scores = np.empty((1, k), dtype=np.float32)
         ids = np.empty((1, k), dtype=np.int64)
         _lib.call("mq_index_search_masked", self._h, _lib.ptr(q), k, _lib.ptr(bits), _lib.ptr(scores),
