@@ -236,6 +236,8 @@ def config4(args, enc, world, rank, dev, backend):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if world > 1:
+        searcher.timings = []
     t0 = time.perf_counter()
     for it in range(args.config4_steps):
         step(evs[it])
@@ -244,6 +246,12 @@ def config4(args, enc, world, rank, dev, backend):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    coll = None
+    if world > 1:
+        coll = {}
+        for tag, nbytes, ms in searcher.resolve_timings():
+            c = coll.setdefault(tag, {"ms_per_step": 0.0, "bytes_per_rank": nbytes})
+            c["ms_per_step"] = round(c["ms_per_step"] + ms / args.config4_steps, 4)
     if world > 1:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -260,7 +268,7 @@ def config4(args, enc, world, rank, dev, backend):
             "steps": args.config4_steps, "n_gpus": world, "scaling": "strong",
             "encoder_ms": round(statistics.mean(e[0].elapsed_time(e[1]) for e in evs), 3),
             "search_ms": round(statistics.mean(e[1].elapsed_time(e[2]) for e in evs), 3),
-            "planted_top1_ok": ok, "screen_fallbacks": fb}
+            "planted_top1_ok": ok, "screen_fallbacks": fb, "allgather_rank0": coll}
 
 
 def _timed_steps(fn, steps, warmup):
@@ -433,6 +441,30 @@ def clustered(args, enc, dev, ids, mask, q):
                                  % (min(B, 100), min(B, 100))}
 
 
+def langchain_embed_documents(args, dev):
+    """LangChain-level `embed_documents` (the call `Chroma.from_documents` makes at
+    src/ingest_medical.py:106-110) through the drop-in at both arithmetics
+    (`HipBertEmbeddings(precision=)`): host strings in (char tokenizer, 30 CJK chars = 32
+    tokens), Python float lists out - tokenisation, H2D / D2H and list building included."""
+    from mediquery_hip import HipBertEmbeddings
+    rng = np.random.default_rng(17)
+    texts = ["".join(chr(c) for c in rng.integers(0x4E00, 0x9FA5, 30)) for _ in range(2048)]
+    out = {}
+    for prec in ("f32", "f32x6"):
+        emb = HipBertEmbeddings(synthetic=True, precision=prec, device=dev.index, batch_size=args.batch)
+        emb.embed_documents(texts[:args.batch])  # warm-up
+        t0 = time.perf_counter()
+        vecs = emb.embed_documents(texts)
+        dt = time.perf_counter() - t0
+        assert len(vecs) == len(texts) and len(vecs[0]) == 768
+        out[prec] = {"docs_per_s": round(len(texts) / dt, 1), "ms_per_batch": round(dt / (len(texts) / args.batch) * 1e3, 3)}
+        del emb
+    torch.cuda.empty_cache()
+    out["note"] = ("%d texts of 30 CJK chars (L = 32 with [CLS]/[SEP]), batches of %d, host strings -> "
+                   "List[List[float]]" % (len(texts), args.batch))
+    return out
+
+
 def workload_name(rows, batch, world):
     """Which BASELINE.json config the sizes are (config 4 = its per-GPU shard at N=1)."""
     if rows == 1_000_000 and batch == 256:
@@ -527,6 +559,8 @@ def main():
         index.read_timing()
         enc.set_timing(True)
         index.set_timing(True)
+        if world > 1:
+            searcher.timings = []  # HIP events around each collective (host time for gloo)
         t0 = time.perf_counter()
         for it in range(args.steps):
             step(evs[it])
@@ -535,6 +569,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        coll = None
+        if world > 1:
+            coll = {}
+            for tag, nbytes, ms in searcher.resolve_timings():
+                c = coll.setdefault(tag, {"ms_per_step": 0.0, "bytes_per_rank": nbytes, "calls": 0})
+                c["ms_per_step"] += ms / args.steps
+                c["calls"] += 1
+            searcher.timings = None
         if world > 1:
             t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -543,7 +585,8 @@ def main():
         stage_ms.update({k: v / args.steps for k, v in index.read_timing().items()})
         enc.set_timing(False)
         index.set_timing(False)
-        return {"elapsed": elapsed, "stage_ms": stage_ms, "screen_fallbacks": index.screen_fallbacks - fb0,
+        return {"elapsed": elapsed, "stage_ms": stage_ms, "collectives": coll,
+                "screen_fallbacks": index.screen_fallbacks - fb0,
                 "screen_passdowns": index.screen_passdowns - pd0,
                 "enc_ms": statistics.mean(e[0].elapsed_time(e[1]) for e in evs),
                 "srch_ms": statistics.mean(e[1].elapsed_time(e[2]) for e in evs)}
@@ -669,7 +712,31 @@ def main():
         extras["long_query_p50"] = long_queries(args, enc, index, dev, K)
         extras["config2"] = config2(args, enc, dev, ids, mask, q)
         extras["clustered_corpus"] = clustered(args, enc, dev, ids, mask, q)
+        extras["langchain_embed_documents"] = langchain_embed_documents(args, dev)
     run_counters = _counters(index)  # every search of the run, timed or not
+
+    dist_info = None
+    if world > 1:
+        # what the collectives ran on, for the driver's SCALE run: the backend, the world
+        # size the process group saw, each rank's bound device, and the headline step's
+        # per-collective time on every rank
+        props = torch.cuda.get_device_properties(local)
+        mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": local,
+                "device_name": props.name, "pci_bus_id": getattr(props, "pci_bus_id", None),
+                "rows": cnt, "row_offset": off,
+                "collectives_ms_per_step": {t: round(c["ms_per_step"], 4)
+                                            for t, c in (runs["f32x6_screen"]["collectives"] or {}).items()}}
+        everyone = [None] * world
+        dist.all_gather_object(everyone, mine)
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "ranks": everyone,
+                     "allgather": {t: {"ms_per_step_rank0": round(c["ms_per_step"], 4),
+                                       "ms_per_step_max": round(max(r["collectives_ms_per_step"].get(t, 0.0)
+                                                                    for r in everyone), 4),
+                                       "bytes_per_rank": c["bytes_per_rank"], "calls_per_step": c["calls"] / args.steps,
+                                       "timer": "HIP events on the launch stream" if dist.get_backend() == "nccl"
+                                       else "host wall time (gloo gathers host copies)"}
+                                   for t, c in (runs["f32x6_screen"]["collectives"] or {}).items()}}
 
     if rank != 0:
         if world > 1:
@@ -781,6 +848,7 @@ def main():
         "split_f32": dict(alt_r, dtype="f32 via exact 3-way bf16 split (6 bf16 MFMAs / product, "
                                        "fp32 accumulate) for the encoder and the direct scan"),
     }
+    out["distributed"] = dist_info
     out["config4_sharded"] = c4
     out["config5_bf16_rerank"] = cfg5
     out["secondary_long_queries"] = sec

@@ -179,11 +179,19 @@ int mq_mask_eval_bits(const int32_t* codes, int64_t n, const uint64_t* lut_words
                       int mode, void* stream);
 int mq_mask_combine(uint32_t* dst, const uint32_t* src, int64_t n_words, int mode, void* stream);
 /* Exact top-k of one query over the allowed rows (same ranking and padding as
- * mq_index_search; bits: a device mask of >= ceil(n / 32) words).  The int8 certified
- * screen runs with the mask; an uncertified query is answered from the allowed rows
- * gathered on the device (counted by mq_index_masked_gathers).  Synchronous. */
+ * mq_index_search; bits: a device mask of >= ceil(n / 32) words on the index's GPU).  The
+ * int8 certified screen runs with the mask; an uncertified query is answered by the
+ * streaming exact scan with the mask (counted by mq_index_masked_gathers).  Synchronous.
+ * The mq_mask_* calls launch on the GPU their buffers live on (`stream` must belong to it).
+ * Replaces Chroma's `similarity_search(filter=)` / `query(where=)` (src/medical_engine.py:52). */
 int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32_t* bits, float* out_scores,
                            int64_t* out_ids, int io_on_device, void* stream);
+/* The same for nq queries at once (queries [nq, dim], outputs [nq, k]; one mask for all) -
+ * Chroma's batched `query(query_embeddings=[...], where=)`.  Batches of > 64 queries with
+ * k <= 16 run the bf16 threshold scan (K9t) with the mask + fp32 re-rank + certificate;
+ * uncertified queries and other batches run the masked streaming exact scan. */
+int mq_index_search_masked_batch(mq_index* ix, const float* queries, int64_t nq, int k, const uint32_t* bits,
+                                 float* out_scores, int64_t* out_ids, int io_on_device, void* stream);
 int mq_index_masked_gathers(const mq_index* ix, int64_t* count);
 
 /* Persistence: a flat binary slab (header + rows); written files are

@@ -313,14 +313,17 @@ __global__ __launch_bounds__(256, KC <= 16 ? 2 : 1) void flat_search_kernel(
 // BF: the rows are the bf16 shadow (half the bytes; a 16-B load carries 8 elements, each
 // widened exactly to fp32 and multiplied with the fp32 query) - the certified screen's
 // single-query scan.
+// MASKED (filtered search): row r is scored only when bit r % 32 of mask word r / 32 is
+// set - the exact scan over the allowed rows with no gather of them.
 constexpr int kStreamMaxNV = 16;  // 16-B loads per lane per row: dim <= 1024
 
-template <int NQ, int KC, int NV, bool BF = false>
+template <int NQ, int KC, int NV, bool BF = false, bool MASKED = false>
 __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restrict__ Q, int nq,
                                                             const float* __restrict__ C,
                                                             int64_t n_rows, int dim, int kl,
                                                             float* __restrict__ cand_s,
-                                                            int* __restrict__ cand_i) {
+                                                            int* __restrict__ cand_i,
+                                                            const unsigned* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float qs[];  // [NQ][dim], zero padded
   const int tid = threadIdx.x, gl = tid & 15;
   for (int i = tid; i < NQ * dim; i += 256) {
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
   const bool owner = gl < nq && gl < NQ;  // lane gl keeps query gl's list
   const float* qbase = qs + gl * EPV;
 
-  auto score_rows = [&](const floatx4 (&v)[2][NV], int64_t r0, int nr)
+  auto score_rows = [&](const floatx4 (&v)[2][NV], int64_t r0, int nr, const unsigned (&mw)[2])
       __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -375,22 +378,25 @@ __global__ __launch_bounds__(256) void stream_search_kernel(const float* __restr
         mine = gl == j ? acc : mine;
       }
       const int64_t r = r0 + u * n_groups;
-      if (u < nr && owner && top.beats_tail(mine, (int)r)) top.insert(mine, (int)r);
+      const bool here = !MASKED || ((mw[u] >> (r & 31)) & 1u);
+      if (u < nr && owner && here && top.beats_tail(mine, (int)r)) top.insert(mine, (int)r);
     }
   };
 
   for (int64_t r0 = group; r0 < n_rows; r0 += 2 * n_groups) {
     const int nr = r0 + n_groups < n_rows ? 2 : 1;
     floatx4 v[2][NV];
+    unsigned mw[2] = {~0u, ~0u};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const floatx4* rp =
-          reinterpret_cast<const floatx4*>(C + (u < nr ? r0 + u * n_groups : r0) * row_words) + gl;
+      const int64_t r = u < nr ? r0 + u * n_groups : r0;
+      const floatx4* rp = reinterpret_cast<const floatx4*>(C + r * row_words) + gl;
 #pragma unroll
       for (int it = 0; it < NV; ++it)
         if (it < nv) v[u][it] = __builtin_nontemporal_load(rp + it * 16);
+      if constexpr (MASKED) mw[u] = mask[r >> 5];
     }
-    score_rows(v, r0, nr);
+    score_rows(v, r0, nr, mw);
   }
   // Block-level merge of the 16 lane groups' lists: one list per (block, query), so K10
   // merges 16x fewer lists (for a single query its 8192-list merge was 78 us).  Lists go
@@ -897,7 +903,10 @@ __global__ __launch_bounds__(kFinT) void i8_finish_kernel(const float* __restric
   __syncthreads();
   MQ_FIN_TS(6);
   if (tid == 0) {
-    const bool cert = ranked && nlive_sh <= kFinLive && nl >= k && tau[q] + e_sh < ek_sh;
+    // fewer than k live rows: exact only when tau = -inf (every row the scan saw survived:
+    // a filter admitting fewer than k rows) - the padded answer is then the whole set
+    const bool cert = ranked && nlive_sh <= kFinLive &&
+                      (nl >= k ? tau[q] + e_sh < ek_sh : tau[q] == -INFINITY);
     if (!cert) fail[atomicAdd(n_fail, 1)] = q;
 #if MQ_FIN_DBG & 16
     printf("FIN cnt %d nl %d dt %llu %llu %llu %llu %llu %llu\n", cnt, nl, tsx[1] - tsx[0], tsx[2] - tsx[1],
@@ -1366,7 +1375,6 @@ struct mq_index {
   DevBuf msel, mblk;     // masked search: the allowed rows (sorted) + per-block counts
   DevBuf mres_s, mres_i;  // masked search: results staged for the host
   PinBuf pin;             // pinned host staging of the host-pointer search calls
-  mq_index* msub = nullptr;  // masked search fallback: the allowed rows gathered
   DevBuf rows8, scale8, err8, stats8;  // int8 shadow [cap, dim] + per-row scales, errors ||c - scale r8|| + maxima (as stats16)
   int64_t n8 = 0;                // rows already mirrored into rows8
   int64_t masked_gathers = 0;    // masked searches the int8 screen could not certify (gathered)
@@ -1468,7 +1476,7 @@ enum ScanKind { SCAN_F32, SCAN_X6, SCAN_BF16, SCAN_STREAM, SCAN_STREAM16 };
 
 template <int NQ, int KC, bool BF>
 void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
-                      int* ci, hipStream_t s) {
+                      int* ci, hipStream_t s, const unsigned* mask) {
   // query image, then the block merge's [16][NQ][KC] (score, id) lists in the same LDS
   const size_t lds = std::max((size_t)NQ * ix->dim * sizeof(float), (size_t)16 * NQ * KC * 8);
   auto launch = [&](auto kern) {
@@ -1476,8 +1484,17 @@ void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int bl
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, q, nq,
-                       BF ? ix->rows16.as<float>() : ix->rows, ix->n, ix->dim, kl, cs, ci);
+                       BF ? ix->rows16.as<float>() : ix->rows, ix->n, ix->dim, kl, cs, ci, mask);
   };
+  if constexpr (!BF) {  // the masked scan reads the fp32 rows
+    if (mask) {
+      if (ix->dim == 768)
+        launch(stream_search_kernel<NQ, KC, 12, false, true>);
+      else
+        launch(stream_search_kernel<NQ, KC, kStreamMaxNV, false, true>);
+      return;
+    }
+  }
   if (ix->dim == 768)  // the dmeta / BERT-base width, register arrays sized exactly
     launch(stream_search_kernel<NQ, KC, BF ? 6 : 12, BF>);
   else
@@ -1486,17 +1503,17 @@ void launch_stream_nq(const mq_index* ix, const float* q, int nq, int kl, int bl
 
 template <int KC, bool BF = false>
 void launch_stream(const mq_index* ix, const float* q, int nq, int kl, int blocks, float* cs,
-                   int* ci, hipStream_t s) {
+                   int* ci, hipStream_t s, const unsigned* mask = nullptr) {
   if (nq <= 1)
-    launch_stream_nq<1, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<1, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s, mask);
   else if (nq <= 2)
-    launch_stream_nq<2, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<2, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s, mask);
   else if (nq <= 4)
-    launch_stream_nq<4, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<4, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s, mask);
   else if (nq <= 8)
-    launch_stream_nq<8, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<8, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s, mask);
   else
-    launch_stream_nq<16, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s);
+    launch_stream_nq<16, KC, BF>(ix, q, nq, kl, blocks, cs, ci, s, mask);
 }
 
 // streaming-kernel grid: up to 2 blocks per CU, at least ~8 rows per lane group
@@ -1541,7 +1558,7 @@ int read_flag(mq_index* ix, const int* dflag, hipStream_t s, int* out) {
 // batch is re-scanned with 64-entry lists, so results are exact either way.  The
 // check costs one 4-byte device->host read, i.e. k > 16 calls are synchronous.
 int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* os, int64_t* oi,
-              hipStream_t s) {
+              hipStream_t s, const unsigned* mask = nullptr) {  // (mask: SCAN_STREAM only)
   // the bf16 scan keeps 8-entry lists whatever k (measured: 16-entry lists cost it ~40%;
   // k > 8 then runs with the merge's overflow check)
   int kc = kind == SCAN_BF16 ? 8 : kc_scan(k);
@@ -1565,9 +1582,9 @@ int scan_topk(mq_index* ix, int kind, const float* q, int64_t nq, int k, float* 
     if (kind == SCAN_STREAM) {
       const int nb = stream_blocks(ix);
       switch (kc) {
-        case 8: launch_stream<8>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
-        case 16: launch_stream<16>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
-        default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s); break;
+        case 8: launch_stream<8>(ix, q, (int)nq, kl, nb, cs, ci, s, mask); break;
+        case 16: launch_stream<16>(ix, q, (int)nq, kl, nb, cs, ci, s, mask); break;
+        default: launch_stream<MQ_MAX_K>(ix, q, (int)nq, kl, nb, cs, ci, s, mask); break;
       }
     } else if (kind == SCAN_STREAM16) {
       const int nb = stream_blocks(ix);
@@ -1648,7 +1665,7 @@ bool thresh_ok(const mq_index* ix, int64_t nq) {
 }
 
 int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, int64_t* oi,
-                hipStream_t s, int tau_rank, int* fail_count, int64_t* fail) {
+                hipStream_t s, int tau_rank, int* fail_count, int64_t* fail, const unsigned* mask = nullptr) {
   const size_t n_lists = 2 * (size_t)ix->num_cus;
   int rc = ix->ts_lmax.ensure(n_lists * nq * sizeof(float));
   if (!rc) rc = ix->ts_tau.ensure(nq * sizeof(float));
@@ -1658,7 +1675,7 @@ int thresh_topk(mq_index* ix, const float* q16, int64_t nq, int kc, float* os, i
   if (rc) return rc;
   ThreshArgs a{q16, (int)nq, ix->rows16.as<unsigned char>(), ix->n, ix->dim, ix->num_cus, kc,
                ix->ts_lmax.as<float>(), ix->ts_tau.as<float>(), ix->ts_count.as<int>(),
-               ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi, tau_rank, fail_count, fail};
+               ix->ts_cs.as<float>(), ix->ts_ci.as<int>(), os, oi, tau_rank, fail_count, fail, mask};
   if (ix->tl.used > 4096) ix->tl.drain();
   launch_thresh(a, s, &ix->tl);
   ix->tl.close(s);
@@ -2161,7 +2178,6 @@ int mq_index_destroy(mq_index* ix) {
     ix->coarse_i.release();
     ix->flag.release();
     ix->stats16.release();
-    if (ix->msub) mq_index_destroy(ix->msub);
     for (DevBuf* b : {&ix->ts_lmax, &ix->ts_tau, &ix->ts_count, &ix->ts_cs, &ix->ts_ci, &ix->i8c_cs,
                       &ix->i8c_ci, &ix->i8c_count, &ix->msel, &ix->mblk, &ix->mres_s, &ix->mres_i, &ix->rows8,
                       &ix->scale8, &ix->err8, &ix->stats8})
@@ -2293,13 +2309,72 @@ int mq_index_select(mq_index* src, const int64_t* rows, int64_t n, mq_index* dst
   return MQ_OK;
 }
 
-// Filtered exact search of one query over the rows whose mask bit is set (Chroma's
-// similarity_search(filter=), src/medical_engine.py:52).  The int8 certified screen (K9q)
-// runs with the mask - masked rows do not exist for its sample, appending pass or
-// certificate, so the answer is exact over the allowed rows; a query it cannot certify
-// (or k > 16, or an index the int8 tier does not apply to) takes the gather path: the
-// allowed rows compacted in order on the device, gathered into a sub-index, scanned
-// exactly (direct fp32), ids mapped back.  Synchronous.
+// Filtered exact search (Chroma's similarity_search(filter=), src/medical_engine.py:52):
+// every row whose mask bit is unset is absent from the scan.  Paths:
+//  * one query: the int8 certified screen (K9q) with the mask - masked rows do not exist
+//    for its sample, appending pass or certificate;
+//  * a batch of > 64 queries (k <= 16): the bf16 threshold scan (K9t) with the mask, fp32
+//    re-rank and certificate, as the unfiltered batched screen;
+//  * what neither certifies, and other batches: the streaming exact fp32 scan (K9s) with
+//    the mask, 16 queries per launch (no gather of the allowed rows);
+//  * dims the streaming scan does not take (dim % 64 != 0): the allowed rows compacted and
+//    gathered into a scratch index that is released after the search.
+// Synchronous.  `masked_gathers` counts the queries the screens did not certify.
+int masked_stream(mq_index* ix, const float* q, int64_t nq, int k, const unsigned* bits, float* os, int64_t* oi,
+                  hipStream_t s) {
+  for (int64_t q0 = 0; q0 < nq; q0 += 16) {
+    const int64_t nn = std::min<int64_t>(16, nq - q0);
+    const int rc = scan_topk(ix, SCAN_STREAM, q + q0 * ix->dim, nn, k, os + q0 * k, oi + q0 * k, s, bits);
+    if (rc) return rc;
+  }
+  return MQ_OK;
+}
+
+int masked_gather(mq_index* ix, const float* q, int k, const unsigned* bits, float* os, int64_t* oi,
+                  hipStream_t s) {
+  const int64_t n_words = (ix->n + 31) / 32;
+  const int nb = (int)((n_words + 255) / 256);
+  int rc = ix->msel.ensure((size_t)ix->n * sizeof(int64_t));
+  if (!rc) rc = ix->mblk.ensure((size_t)(nb + 1) * sizeof(int));
+  if (rc) return rc;
+  int* blk = ix->mblk.as<int>();
+  hipLaunchKernelGGL(mask_count_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk);
+  hipLaunchKernelGGL(mask_scan_kernel, dim3(1), dim3(256), 0, s, blk, nb);
+  hipLaunchKernelGGL(mask_compact_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk, ix->msel.as<int64_t>());
+  MQ_HIP(hipGetLastError());
+  int count = 0;
+  rc = read_flag(ix, blk + nb, s, &count);
+  if (rc) return rc;
+  if (count == 0) return fill_padding(os, oi, k, s);
+  mq_index* sub = nullptr;
+  rc = mq_index_create(ix->device, ix->dim, 0, ix->dtype, &sub);
+  if (rc) return rc;
+  rc = reserve_rows(sub, count, s);
+  if (!rc) {
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((count + 3) / 4)), dim3(256), 0, s, ix->rows,
+                       ix->msel.as<int64_t>(), (int64_t)count, ix->dim, sub->rows);
+    if (hipGetLastError() != hipSuccess) rc = MQ_EHIP;
+  }
+  sub->n = count;
+  const int kk = (int)std::min<int64_t>(k, count);
+  if (!rc && kk < k) rc = fill_padding(os, oi, k, s);
+  if (!rc) rc = ix->out_s.ensure((size_t)k * 4);
+  if (!rc) rc = ix->out_i.ensure((size_t)k * 8);
+  // (kk results into scratch, then into the first kk slots)
+  if (!rc) rc = search_direct(sub, q, 1, kk, ix->out_s.as<float>(), ix->out_i.as<int64_t>(), s);
+  if (!rc) {
+    hipLaunchKernelGGL(remap_ids_kernel, dim3(1), dim3(256), 0, s, ix->out_i.as<int64_t>(), (int64_t)kk,
+                       ix->msel.as<int64_t>());
+    if (hipGetLastError() != hipSuccess) rc = MQ_EHIP;
+  }
+  if (!rc && hipMemcpyAsync(os, ix->out_s.p, (size_t)kk * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) rc = MQ_EHIP;
+  if (!rc && hipMemcpyAsync(oi, ix->out_i.p, (size_t)kk * 8, hipMemcpyDeviceToDevice, s) != hipSuccess) rc = MQ_EHIP;
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = MQ_EHIP;
+  mq_index_destroy(sub);  // the gathered copy is not kept (a wide filter's copy would rival the slab)
+  if (rc == MQ_EHIP) MQ_FAIL(MQ_EHIP, "masked gather search failed");
+  return rc;
+}
+
 int search_masked(mq_index* ix, const float* q, int k, const unsigned* bits, float* os, int64_t* oi,
                   hipStream_t s) {
   if (ix->n == 0) return fill_padding(os, oi, k, s);
@@ -2322,52 +2397,88 @@ int search_masked(mq_index* ix, const float* q, int k, const unsigned* bits, flo
     if (n_fail == 0) return MQ_OK;
     ix->masked_gathers++;
   }
-  // gather path
-  const int64_t n_words = (ix->n + 31) / 32;
-  const int nb = (int)((n_words + 255) / 256);
-  int rc = ix->msel.ensure((size_t)ix->n * sizeof(int64_t));
-  if (!rc) rc = ix->mblk.ensure((size_t)(nb + 1) * sizeof(int));
-  if (rc) return rc;
-  int* blk = ix->mblk.as<int>();
-  hipLaunchKernelGGL(mask_count_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk);
-  hipLaunchKernelGGL(mask_scan_kernel, dim3(1), dim3(256), 0, s, blk, nb);
-  hipLaunchKernelGGL(mask_compact_kernel, dim3(nb), dim3(256), 0, s, bits, ix->n, blk, ix->msel.as<int64_t>());
-  MQ_HIP(hipGetLastError());
-  int count = 0;
-  rc = read_flag(ix, blk + nb, s, &count);
-  if (rc) return rc;
-  if (count == 0) return fill_padding(os, oi, k, s);
-  if (!ix->msub) {
-    rc = mq_index_create(ix->device, ix->dim, 0, ix->dtype, &ix->msub);
+  if (stream_ok(ix)) {
+    const int rc = masked_stream(ix, q, 1, k, bits, os, oi, s);
     if (rc) return rc;
+    MQ_HIP(hipStreamSynchronize(s));
+    return MQ_OK;
   }
-  mq_index* sub = ix->msub;
-  sub->n = 0;  // (nothing of the previous filter's rows is kept)
-  rc = reserve_rows(sub, count, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((count + 3) / 4)), dim3(256), 0, s, ix->rows,
-                     ix->msel.as<int64_t>(), (int64_t)count, ix->dim, sub->rows);
-  MQ_HIP(hipGetLastError());
-  sub->n = count;
-  sub->n16 = sub->n8 = 0;
-  const int kk = (int)std::min<int64_t>(k, count);
-  if (kk < k) {
-    rc = fill_padding(os, oi, k, s);
+  return masked_gather(ix, q, k, bits, os, oi, s);
+}
+
+int search_masked_batch(mq_index* ix, const float* q, int64_t nq, int k, const unsigned* bits, float* os,
+                        int64_t* oi, hipStream_t s) {
+  if (ix->n == 0) return fill_padding(os, oi, nq * k, s);
+  if (nq == 1) return search_masked(ix, q, k, bits, os, oi, s);
+  const bool exact_kind = ix->precision == MQ_DTYPE_F32_SCREEN || ix->precision == MQ_DTYPE_F32;
+  if (!stream_ok(ix)) {  // (dim % 64 != 0: no masked scan kernel takes it)
+    for (int64_t j = 0; j < nq; ++j) {
+      const int rc = search_masked(ix, q + j * ix->dim, k, bits, os + j * k, oi + j * k, s);
+      if (rc) return rc;
+    }
+    return MQ_OK;
+  }
+  if (!(exact_kind && k <= kScreenMaxK && thresh_ok(ix, nq) && ix->dim <= 1024)) {
+    const int rc = masked_stream(ix, q, nq, k, bits, os, oi, s);
     if (rc) return rc;
+    MQ_HIP(hipStreamSynchronize(s));
+    return MQ_OK;
   }
-  rc = ix->out_s.ensure((size_t)k * 4);
-  if (!rc) rc = ix->out_i.ensure((size_t)k * 8);
+  // the batched bf16 screen with the mask (search_screened's TIER_BF16, synchronous)
+  const int kc = (int)std::min<int64_t>(MQ_MAX_K, ix->n);
+  int rc = ensure_shadow(ix, s);
+  if (!rc) rc = queries_to_bf16(ix, q, nq, s);
+  if (!rc) rc = ix->coarse_s.ensure((size_t)nq * kc * sizeof(float));
+  if (!rc) rc = ix->coarse_i.ensure((size_t)nq * kc * sizeof(int64_t));
+  if (!rc) rc = ix->flag.ensure(sizeof(int));
+  if (!rc) rc = ix->tier_fail[TIER_BF16].ensure((size_t)nq * sizeof(int64_t));
   if (rc) return rc;
-  // (kk results into scratch, then into the first kk slots)
-  rc = search_direct(sub, q, 1, kk, ix->out_s.as<float>(), ix->out_i.as<int64_t>(), s);
+  rc = thresh_topk(ix, ix->q16.as<float>(), nq, kc, ix->coarse_s.as<float>(), ix->coarse_i.as<int64_t>(), s,
+                   kTsRank, nullptr, nullptr, bits);
   if (rc) return rc;
-  hipLaunchKernelGGL(remap_ids_kernel, dim3(1), dim3(256), 0, s, ix->out_i.as<int64_t>(), (int64_t)kk,
-                     ix->msel.as<int64_t>());
+  const unsigned* stats = ix->stats16.as<unsigned>();
+  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)nq), dim3(256), 0, s, q, ix->rows, ix->dim,
+                     ix->coarse_i.as<int64_t>(), kc, k, os, oi, ix->coarse_s.as<float>(), VERIFY_BF16_Q16, stats);
+  MQ_HIP(hipMemsetAsync(ix->flag.p, 0, sizeof(int), s));
+  int64_t* fail = ix->tier_fail[TIER_BF16].as<int64_t>();
+  hipLaunchKernelGGL(screen_verify_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, q, ix->dim,
+                     ix->coarse_s.as<float>(), kc, os, k, nq, VERIFY_BF16_Q16, stats, ix->flag.as<int>(), fail,
+                     nullptr);
   MQ_HIP(hipGetLastError());
-  MQ_HIP(hipMemcpyAsync(os, ix->out_s.p, (size_t)kk * 4, hipMemcpyDeviceToDevice, s));
-  MQ_HIP(hipMemcpyAsync(oi, ix->out_i.p, (size_t)kk * 8, hipMemcpyDeviceToDevice, s));
+  int n_fail = 0;
+  rc = read_flag(ix, ix->flag.as<int>(), s, &n_fail);
+  if (rc) return rc;
+  if (n_fail > 0) {  // uncertified: the masked exact scan, results scattered back
+    ix->masked_gathers += n_fail;
+    rc = ix->tier_q[TIER_BF16].ensure((size_t)n_fail * ix->dim * sizeof(float));
+    if (!rc) rc = ix->tier_s[TIER_BF16].ensure((size_t)n_fail * k * sizeof(float));
+    if (!rc) rc = ix->tier_i[TIER_BF16].ensure((size_t)n_fail * k * sizeof(int64_t));
+    if (rc) return rc;
+    float* sq = ix->tier_q[TIER_BF16].as<float>();
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n_fail + 3) / 4)), dim3(256), 0, s, q, fail,
+                       (int64_t)n_fail, ix->dim, sq);
+    MQ_HIP(hipGetLastError());
+    rc = masked_stream(ix, sq, n_fail, k, bits, ix->tier_s[TIER_BF16].as<float>(),
+                       ix->tier_i[TIER_BF16].as<int64_t>(), s);
+    if (rc) return rc;
+    const int64_t total = (int64_t)n_fail * k;
+    hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       ix->tier_s[TIER_BF16].as<float>(), ix->tier_i[TIER_BF16].as<int64_t>(), fail,
+                       (int64_t)n_fail, k, os, oi);
+    MQ_HIP(hipGetLastError());
+  }
   MQ_HIP(hipStreamSynchronize(s));
   return MQ_OK;
+}
+
+// Device of a pointer (HIP device memory), or -1 (host / unknown).
+int pointer_device(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return a.type == hipMemoryTypeDevice ? a.device : -1;
 }
 
 int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut, uint32_t* bits, int mode,
@@ -2377,6 +2488,10 @@ int mq_mask_eval(const int32_t* codes, int64_t n, const uint8_t* lut, int n_lut,
   MQ_CHECK_ARG(mode == MQ_MASK_SET || mode == MQ_MASK_AND || mode == MQ_MASK_OR, "bad mask mode %d", mode);
   if (n == 0) return MQ_OK;
   MQ_CHECK_ARG(codes && lut && bits, "NULL buffer");
+  const int dev = pointer_device(bits);
+  MQ_CHECK_ARG(dev >= 0 && pointer_device(codes) == dev && pointer_device(lut) == dev,
+               "codes, lut and bits must be device memory of one GPU");
+  DeviceGuard dg(dev);  // the launch runs on the buffers' GPU (stream: that device's)
   hipLaunchKernelGGL(mask_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      (const int*)codes, n, (const unsigned char*)lut, LutWords{}, n_lut, (unsigned*)bits, mode);
   MQ_HIP(hipGetLastError());
@@ -2391,6 +2506,9 @@ int mq_mask_eval_bits(const int32_t* codes, int64_t n, const uint64_t* lut_words
   MQ_CHECK_ARG(lut_words, "NULL table");
   if (n == 0) return MQ_OK;
   MQ_CHECK_ARG(codes && bits, "NULL buffer");
+  const int dev = pointer_device(bits);
+  MQ_CHECK_ARG(dev >= 0 && pointer_device(codes) == dev, "codes and bits must be device memory of one GPU");
+  DeviceGuard dg(dev);
   LutWords lw{};
   for (int i = 0; i < (n_lut + 63) / 64; ++i) lw.w[i] = lut_words[i];
   hipLaunchKernelGGL(mask_eval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
@@ -2405,38 +2523,40 @@ int mq_mask_combine(uint32_t* dst, const uint32_t* src, int64_t n_words, int mod
   MQ_CHECK_ARG(mode >= MQ_MASK_SET && mode <= MQ_MASK_CLEAR, "bad mask mode %d", mode);
   if (n_words == 0) return MQ_OK;
   MQ_CHECK_ARG(dst, "NULL dst");
+  const int dev = pointer_device(dst);
+  MQ_CHECK_ARG(dev >= 0 && (!src || pointer_device(src) == dev), "dst and src must be device memory of one GPU");
+  DeviceGuard dg(dev);
   hipLaunchKernelGGL(mask_combine_kernel, dim3((unsigned)((n_words + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, (unsigned*)dst, (const unsigned*)src, n_words, mode);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
 
-int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32_t* bits, float* out_scores,
-                           int64_t* out_ids, int io_on_device, void* stream) {
+int mq_index_search_masked_batch(mq_index* ix, const float* queries, int64_t nq, int k, const uint32_t* bits,
+                                 float* out_scores, int64_t* out_ids, int io_on_device, void* stream) {
   clear_error();
   MQ_CHECK_ARG(ix, "NULL index");
+  MQ_CHECK_ARG(nq >= 0 && nq <= (1ll << 24), "query count %lld out of range", (long long)nq);
   MQ_CHECK_ARG(k >= 1 && k <= MQ_MAX_K, "k must be in [1, %d] (got %d)", MQ_MAX_K, k);
-  MQ_CHECK_ARG(query && bits && out_scores && out_ids, "NULL buffer");
+  if (nq == 0) return MQ_OK;
+  MQ_CHECK_ARG(queries && bits && out_scores && out_ids, "NULL buffer");
   std::lock_guard<std::mutex> lk(ix->mu);
+  MQ_CHECK_ARG(pointer_device(bits) == ix->device, "the mask must be device memory of the index's GPU %d",
+               ix->device);
   DeviceGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
-  if (io_on_device) {
-    const int rc = search_masked(ix, query, k, (const unsigned*)bits, out_scores, out_ids, s);
-    if (rc) return rc;
-    MQ_HIP(hipStreamSynchronize(s));
-    return MQ_OK;
-  }
-  const size_t qb = (size_t)ix->dim * 4, sb = (size_t)k * 4, ib = (size_t)k * 8;
+  if (io_on_device) return search_masked_batch(ix, queries, nq, k, (const unsigned*)bits, out_scores, out_ids, s);
+  const size_t qb = (size_t)nq * ix->dim * 4, sb = (size_t)nq * k * 4, ib = (size_t)nq * k * 8;
   int rc = ix->stage.ensure(qb);
   if (!rc) rc = ix->mres_s.ensure(sb);
   if (!rc) rc = ix->mres_i.ensure(ib);
   if (!rc) rc = ix->pin.ensure(qb + sb + ib);  // pinned staging (see mq_index_search)
   if (rc) return rc;
   unsigned char* hp = ix->pin.as<unsigned char>();
-  memcpy(hp, query, qb);
+  memcpy(hp, queries, qb);
   MQ_HIP(hipMemcpyAsync(ix->stage.p, hp, qb, hipMemcpyHostToDevice, s));
-  rc = search_masked(ix, ix->stage.as<float>(), k, (const unsigned*)bits, ix->mres_s.as<float>(),
-                     ix->mres_i.as<int64_t>(), s);
+  rc = search_masked_batch(ix, ix->stage.as<float>(), nq, k, (const unsigned*)bits, ix->mres_s.as<float>(),
+                           ix->mres_i.as<int64_t>(), s);
   if (rc) return rc;
   MQ_HIP(hipMemcpyAsync(hp + qb, ix->mres_s.p, sb, hipMemcpyDeviceToHost, s));
   MQ_HIP(hipMemcpyAsync(hp + qb + sb, ix->mres_i.p, ib, hipMemcpyDeviceToHost, s));
@@ -2444,6 +2564,11 @@ int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32
   memcpy(out_scores, hp + qb, sb);
   memcpy(out_ids, hp + qb + sb, ib);
   return MQ_OK;
+}
+
+int mq_index_search_masked(mq_index* ix, const float* query, int k, const uint32_t* bits, float* out_scores,
+                           int64_t* out_ids, int io_on_device, void* stream) {
+  return mq_index_search_masked_batch(ix, query, 1, k, bits, out_scores, out_ids, io_on_device, stream);
 }
 
 int mq_index_masked_gathers(const mq_index* ix, int64_t* count) {

@@ -75,11 +75,16 @@ __device__ __forceinline__ void glds16(const void* base, unsigned voff, unsigned
       : "memory");
 }
 
-template <int NCH, int MODE>
+// MASKED (batched filtered search): a 32-row block's rows are bits 0..31 of mask word j
+// (block j); a masked row is absent from both passes.  The word is read by a scalar load
+// waited at once at the top of the block (asm: a compiler-visible SMEM load outstanding
+// across the chain would turn its counted LDS waits into lgkmcnt(0)).
+template <int NCH, int MODE, bool MASKED = false>
 __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
     const uint4* __restrict__ Qb, int nq, const unsigned char* __restrict__ C, int64_t n_rows,
     int64_t n_blocks, int period, const float* __restrict__ tau, float* __restrict__ lmax,
-    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci) {
+    int* __restrict__ count, float* __restrict__ cs, int* __restrict__ ci,
+    const unsigned* __restrict__ mask) {
   constexpr int ROW_B = NCH * 128;             // bf16 row bytes
   constexpr int BLK_B = kTsRows * ROW_B;       // one staged block (the shadow is padded to
                                                // whole blocks: no row clamping)
@@ -147,6 +152,11 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   }
   const bool active = qw0 < nq;
   for (int i = 0; i < nb; ++i) {
+    unsigned mw = ~0u;  // (MASKED) block i's row bits
+    if constexpr (MASKED) {
+      const unsigned* mp = mask + (first + (int64_t)i * stride);
+      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(mw) : "s"(mp) : "memory");
+    }
     // own DMAs of block i landed (block i+1's may still fly), then everyone's, and every
     // wave is done reading block i-1, whose buffer this iteration refills
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_WAVE) : "memory");
@@ -191,7 +201,8 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t row = row0 + acc_row(0, e, lane);
-        if (full || row < n_rows) mx = fmaxf(mx, acc[e]);
+        const bool here = !MASKED || ((mw >> acc_row(0, e, lane)) & 1u);
+        if ((full || row < n_rows) && here) mx = fmaxf(mx, acc[e]);
       }
     } else {
       // survivors go to this wave's LDS list (a ballot + lane prefix picks the slots);
@@ -199,12 +210,13 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
       // vmcnt(0) would drain the ring - ever runs inside it
       bool any = false;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) any |= acc[e] >= t;
+      for (int e = 0; e < 16; ++e) any |= acc[e] >= t && (!MASKED || ((mw >> acc_row(0, e, lane)) & 1u));
       if (__builtin_amdgcn_ballot_w64(any && qvalid)) {  // rare: ~128 survivors per query
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int64_t row = row0 + acc_row(0, e, lane);
-          const bool hit = acc[e] >= t && row < n_rows && qvalid;
+          const bool hit = acc[e] >= t && row < n_rows && qvalid &&
+                           (!MASKED || ((mw >> acc_row(0, e, lane)) & 1u));
           const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
           if (m) {
             const int pos = n_surv + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
@@ -324,7 +336,7 @@ __global__ __launch_bounds__(256) void bf16_select_kernel(const float* __restric
   }
 }
 
-template <int NCH>
+template <int NCH, bool MASKED>
 void launch_nch(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   // One workgroup per CU in total (LDS and VGPRs allow one): several query groups split
   // the CUs instead of running in rounds.  G is a multiple of the 8 XCDs, so (x, y) and
@@ -335,25 +347,33 @@ void launch_nch(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   const int64_t n_blocks = (a.n + kTsRows - 1) / kTsRows;
   const uint4* qb = reinterpret_cast<const uint4*>(a.q16);
   tl->mark(s, 0);
-  hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_MAX>), dim3(G, gy), dim3(512), 0, s, qb, a.nq, a.rows,
-                     a.n, n_blocks, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci);
+  hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_MAX, MASKED>), dim3(G, gy), dim3(512), 0, s, qb, a.nq, a.rows,
+                     a.n, n_blocks, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.mask);
   tl->mark(s, 1);
   hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, 2 * G, a.nq,
                      a.tau_rank, a.tau, a.count);
   tl->mark(s, 0);
-  hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_APPEND>), dim3(G, gy), dim3(512), 0, s, qb, a.nq,
-                     a.rows, a.n, n_blocks, 1, a.tau, a.lmax, a.count, a.cs, a.ci);
+  hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_APPEND, MASKED>), dim3(G, gy), dim3(512), 0, s, qb, a.nq,
+                     a.rows, a.n, n_blocks, 1, a.tau, a.lmax, a.count, a.cs, a.ci, a.mask);
   tl->mark(s, 1);
   hipLaunchKernelGGL(bf16_select_kernel, dim3(a.nq), dim3(256), 0, s, a.cs, a.ci, a.count, a.tau, a.kc,
                      a.out_s, a.out_i, a.fail_count, a.fail);
 }
 
-void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
+template <bool MASKED>
+void launch_dim(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   switch (a.dim / 64) {
-    case 4: launch_nch<4>(a, s, tl); break;
-    case 8: launch_nch<8>(a, s, tl); break;
-    default: launch_nch<12>(a, s, tl); break;
+    case 4: launch_nch<4, MASKED>(a, s, tl); break;
+    case 8: launch_nch<8, MASKED>(a, s, tl); break;
+    default: launch_nch<12, MASKED>(a, s, tl); break;
   }
+}
+
+void launch_thresh(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
+  if (a.mask)
+    launch_dim<true>(a, s, tl);
+  else
+    launch_dim<false>(a, s, tl);
 }
 
 // ============================ K9q: int8 threshold scan (few-query screens) ==========

@@ -29,6 +29,9 @@ struct ThreshArgs {
   int tau_rank;               // tau = the tau_rank-th largest sample list maximum (>= tau_rank survivors)
   int* fail_count;            // optional: queries with more than kTsCap or fewer than kc survivors
   int64_t* fail;              //   are appended to fail[] (count in *fail_count, zeroed by the caller)
+  // optional row mask (batched filtered search): bit r % 32 of word r / 32 set = row r
+  // exists; masked rows are skipped by both passes (>= ceil(n / 32) words)
+  const unsigned* mask = nullptr;
 };
 
 // Enqueue the four K9t launches on `s`; timeline stage 0 = the two scans, 1 = tau + select.

@@ -86,6 +86,7 @@ SIGNATURES = {
     "mq_mask_eval_bits": (_I, [_P, _I64, _P, _I, _P, _I, _P]),
     "mq_mask_combine": (_I, [_P, _P, _I64, _I, _P]),
     "mq_index_search_masked": (_I, [_P, _P, _I, _P, _P, _P, _I, _P]),
+    "mq_index_search_masked_batch": (_I, [_P, _P, _I64, _I, _P, _P, _P, _I, _P]),
     "mq_index_masked_gathers": (_I, [_P, ctypes.POINTER(_I64)]),
     "mq_topk_merge_host": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P]),
     "mq_topk_merge_device": (_I, [_P, _P, _I, _I64, _I, _I, _P, _P, _P]),
@@ -160,6 +161,26 @@ def ptr(a):
     if hasattr(a, "data_ptr"):
         return ctypes.c_void_p(a.data_ptr())
     return ctypes.c_void_p(a.ctypes.data)
+
+
+class device_scope:
+    """`with device_scope(d):` makes cuda:d torch's current device (so stream_handle(None)
+    is that device's current stream) - a no-op without torch / CUDA or for d None."""
+
+    def __init__(self, device):
+        self._ctx = None
+        if device is not None and torch is not None and torch.cuda.is_available():
+            self._ctx = torch.cuda.device(int(device))
+
+    def __enter__(self):
+        if self._ctx is not None:
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            return self._ctx.__exit__(*exc)
+        return False
 
 
 def stream_handle(stream=None):

@@ -14,6 +14,8 @@ Scoring needs no communication; the exchanged bytes are nq*k*12 per rank.
 config 4's 8 shards on fewer GPUs than shards): per-shard K9 searches, then the device
 merge (K10) - the exchange step without the collective.
 """
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -52,11 +54,17 @@ class LocalShards:
     reference store being scaled is the Chroma collection of src/medical_engine.py:52).
     Shard s holds rows `shard_bounds(n, n_shards, s)` of what `add_device` receives
     (global id = `base` + shard offset + local id); a search runs K9 on every shard into
-    one [n_shards, nq, k] candidate buffer and merges it on the device (K10)."""
+    one [n_shards, nq, k] candidate buffer and merges it on the device (K10).
 
-    def __init__(self, n_shards, dim=768, device=0, base=0):
+    `index_factory(capacity) -> index` builds one shard (default: a `FlatIndex` on
+    `device`); any object with FlatIndex's add_device / search_device / set_precision /
+    close / __len__ serves, so the CPU tests drive this partition with an oracle shard.
+    Candidates on the host are merged by `merge_topk_host` (the same merge, in C)."""
+
+    def __init__(self, n_shards, dim=768, device=0, base=0, index_factory=None):
         self.n_shards, self.dim, self.device, self.base = int(n_shards), dim, device, int(base)
-        self.shards = [FlatIndex(dim=dim, device=device) for _ in range(self.n_shards)]
+        self._factory = index_factory or (lambda cap: FlatIndex(dim=dim, capacity=cap, device=device))
+        self.shards = [self._factory(0) for _ in range(self.n_shards)]
         self.offsets = [0] * self.n_shards
         self._cand = None
 
@@ -74,7 +82,7 @@ class LocalShards:
             self.offsets[s] = off
             if cnt:  # sized to the shard up front: no re-allocation while adding
                 self.shards[s].close()
-                self.shards[s] = FlatIndex(dim=self.dim, capacity=cnt, device=self.device)
+                self.shards[s] = self._factory(cnt)
                 self.shards[s].add_device(rows[off:off + cnt].contiguous())
 
     def set_precision(self, dtype):
@@ -95,7 +103,12 @@ class LocalShards:
         for s, ix in enumerate(self.shards):
             ix.search_device(queries, k, cs[s], ci[s])
         gi = torch.where(ci >= 0, ci + offs, ci)
-        merge_topk_device(cs, gi, k, out_scores, out_ids)
+        if cs.is_cuda:
+            merge_topk_device(cs, gi, k, out_scores, out_ids)
+        else:
+            ms, mi = merge_topk_host(cs.numpy(), gi.numpy(), k)
+            out_scores.copy_(torch.from_numpy(ms))
+            out_ids.copy_(torch.from_numpy(mi))
         return out_scores, out_ids
 
 
@@ -108,8 +121,14 @@ class ShardedSearcher:
         self.local_search = local_search
         self.offset = int(offset)
         self.group = group
+        # set to a list to time every collective: entries (tag, bytes per rank, ms), where
+        # ms is HIP-event time on the launching stream for RCCL on device tensors (the
+        # collective's stream is joined to it both ways) and host wall time for gloo;
+        # the RCCL events stay pending until `resolve_timings()`
+        self.timings = None
+        self._pending = []
 
-    def _all_gather(self, t):
+    def _all_gather(self, t, tag="gather"):
         """[...] per rank -> [world, ...]: ONE all_gather_into_tensor into a concatenated
         [world * n, ...] buffer (the form both RCCL and gloo accept, so the CPU tests run
         the very call the RCCL path makes), viewed rank-major."""
@@ -117,15 +136,36 @@ class ShardedSearcher:
         t = t.contiguous()
         # RCCL gathers device tensors over xGMI; gloo (CPU tests, or several ranks sharing
         # one GPU in a rehearsal) gathers host copies
-        src = t if dist.get_backend(self.group) == "nccl" else t.cpu()
+        rccl = dist.get_backend(self.group) == "nccl"
+        src = t if rccl else t.cpu()
         flat = src.reshape((-1,) + tuple(src.shape[1:])) if src.dim() else src.reshape(1)
         out = torch.empty((world * flat.shape[0],) + tuple(flat.shape[1:]), dtype=src.dtype, device=src.device)
+        timed = self.timings is not None
+        nbytes = flat.numel() * flat.element_size()
+        if timed and src.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        elif timed:
+            h0 = time.perf_counter()
         dist.all_gather_into_tensor(out, flat, group=self.group)
+        if timed and src.is_cuda:
+            e1.record()
+            self._pending.append((tag, nbytes, e0, e1))
+        elif timed:
+            self.timings.append((tag, nbytes, (time.perf_counter() - h0) * 1e3))
         return out.view((world,) + tuple(t.shape)).to(t.device)
+
+    def resolve_timings(self):
+        """Turn the recorded RCCL events into `timings` entries (synchronises on them)."""
+        for tag, nbytes, e0, e1 in self._pending:
+            e1.synchronize()
+            self.timings.append((tag, nbytes, e0.elapsed_time(e1)))
+        self._pending = []
+        return self.timings
 
     def gather_queries(self, q_local):
         """[B, dim] per rank -> [world*B, dim] on every rank (rank-major)."""
-        g = self._all_gather(q_local)
+        g = self._all_gather(q_local, "queries")
         return g.reshape(-1, q_local.shape[-1])
 
     def search(self, queries, k, keep=None):
@@ -134,7 +174,7 @@ class ShardedSearcher:
         s, i = self.local_search(queries, k)
         if self.offset:
             i = torch.where(i >= 0, i + self.offset, i)
-        gs, gi = unpack_candidates(self._all_gather(pack_candidates(s, i)))  # [world, nq, k]
+        gs, gi = unpack_candidates(self._all_gather(pack_candidates(s, i), "candidates"))  # [world, nq, k]
         if keep is not None:
             gs, gi = gs[:, keep[0]:keep[1]].contiguous(), gi[:, keep[0]:keep[1]].contiguous()
         nq = gs.shape[1]
@@ -155,7 +195,7 @@ class ShardedSearcher:
         rank = dist.get_rank(self.group)
         B = int(q_local.shape[0])
         if sizes is None:
-            sizes = self._all_gather(torch.tensor([B], dtype=torch.int64, device=q_local.device))
+            sizes = self._all_gather(torch.tensor([B], dtype=torch.int64, device=q_local.device), "sizes")
             sizes = [int(x) for x in sizes.reshape(-1).tolist()]
         elif len(sizes) != dist.get_world_size(self.group) or sizes[rank] != B:
             raise ValueError("sizes %s do not match world size / this rank's batch %d" % (sizes, B))
@@ -163,7 +203,7 @@ class ShardedSearcher:
         if Bmax != B:
             pad = torch.zeros((Bmax - B, q_local.shape[1]), dtype=q_local.dtype, device=q_local.device)
             q_local = torch.cat([q_local, pad])
-        g = self._all_gather(q_local)  # [world, Bmax, dim]
+        g = self._all_gather(q_local, "queries")  # [world, Bmax, dim]
         if any(b != Bmax for b in sizes):
             allq = torch.cat([g[r, :b] for r, b in enumerate(sizes)])
         else:

@@ -23,11 +23,21 @@ Weights and vocabulary are never downloaded.  They come, in this order, from:
 Otherwise the constructor raises.  Seeded random weights with the char tokenizer (tests,
 benchmarks) must be asked for explicitly with `synthetic=True`: a silently random encoder
 would hand the Retrieve node semantically random documents.
+
+Arithmetic (`precision=`): "f32x6" (the default, so the
+reference's unchanged `OllamaEmbeddings(model=...)` line at src/medical_engine.py:43 and
+src/ingest_medical.py:104 gets the headline configuration) splits every fp32 operand of the
+batched GEMMs exactly into three bf16 planes and sums six bf16 MFMA products in fp32 -
+fp32-class results (error within 3x of exact fp32 against float64, same parity tolerances);
+"f32" runs the exact fp32 MFMA.  Single queries and other few-row batches run exact fp32
+either way (the split does not pay when the weights, not the MFMAs, bound the launch).
+$MQ_ENCODER_PRECISION sets the default for constructors that do not pass it.
 """
 import os
 
 import numpy as np
 
+from . import _lib
 from .compat import EmbeddingsBase
 from .config import BertConfig, DMETA_BASE
 from .gguf import bert_from_gguf, resolve_ollama_model
@@ -38,6 +48,9 @@ from .weights import load_safetensors
 ENV_WEIGHTS = "MQ_WEIGHTS_PATH"
 ENV_VOCAB = "MQ_VOCAB_FILE"
 ENV_GGUF = "MQ_GGUF_PATH"
+ENV_PRECISION = "MQ_ENCODER_PRECISION"
+PRECISIONS = {"f32": _lib.MQ_DTYPE_F32, "f32x6": _lib.MQ_DTYPE_F32X6}
+DEFAULT_PRECISION = "f32x6"
 
 
 class HipBertEmbeddings(EmbeddingsBase):
@@ -53,11 +66,16 @@ class HipBertEmbeddings(EmbeddingsBase):
                   tanh, llama.cpp's) and vocab; `config` overrides the derived config.
     synthetic:    True = seeded random weights + the deterministic char tokenizer
                   (`seed`); the only way to get them.
+    precision:    "f32x6" (default; $MQ_ENCODER_PRECISION) or "f32" - module doc.
     """
 
     def __init__(self, model="shaw/dmeta-embedding-zh", *, weights_path=None, vocab_file=None,
                  gguf_path=None, synthetic=False, config: BertConfig = None, seed=0, device=0,
-                 batch_size=256, max_length=512, **kwargs):
+                 batch_size=256, max_length=512, precision=None, **kwargs):
+        precision = precision or os.environ.get(ENV_PRECISION) or DEFAULT_PRECISION
+        if precision not in PRECISIONS:
+            raise ValueError("precision must be one of %s, got %r" % (sorted(PRECISIONS), precision))
+        self.precision = precision
         self.model = model
         self.device = device
         self.batch_size = int(batch_size)
@@ -102,6 +120,7 @@ class HipBertEmbeddings(EmbeddingsBase):
         self.max_length = min(int(max_length), config.max_positions)
         self.weights_path, self.vocab_file, self.gguf_path = weights_path, vocab_file, gguf_path
         self.encoder = Encoder(config, weights=weights, seed=seed, device=device)
+        self.encoder.set_precision(PRECISIONS[precision])
         if vocab_file:  # C++ tokenizers of libmqhip.so
             self.tokenizer = NativeTokenizer.wordpiece(vocab_file, max_length=self.max_length)
         elif vocab_tokens is not None:

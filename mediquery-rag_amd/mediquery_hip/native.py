@@ -164,17 +164,21 @@ class FlatIndex:
     def load(self, path):
         _lib.call("mq_index_load", self._h, str(path).encode())
 
-    def search_masked(self, query, k, bits):
-        """Exact top-k of one query over the rows allowed by `bits` (a device mask tensor of
-        >= ceil(n / 32) int32 words, bit r % 32 of word r / 32 = row r; mask_eval builds it)."""
-        q = np.ascontiguousarray(query, dtype=np.float32).reshape(self.dim)
-        if not (getattr(bits, "is_cuda", False) and bits.element_size() == 4 and bits.is_contiguous()
-                and bits.numel() >= (len(self) + 31) // 32):
-            raise ValueError("bits must be a contiguous 32-bit device tensor of >= ceil(n / 32) words")
-        scores = np.empty((1, k), dtype=np.float32)
-        ids = np.empty((1, k), dtype=np.int64)
-        _lib.call("mq_index_search_masked", self._h, _lib.ptr(q), k, _lib.ptr(bits), _lib.ptr(scores),
-                  _lib.ptr(ids), 0, _lib.stream_handle(None))
+    def _check_bits(self, bits):
+        check_mask_words(bits, len(self), self.device)
+
+    def search_masked(self, queries, k, bits):
+        """Exact top-k of each query ([dim] or [nq, dim] host floats) over the rows allowed
+        by `bits` (a device mask tensor on this index's GPU of >= ceil(n / 32) int32 words,
+        bit r % 32 of word r / 32 = row r; mask_eval builds it).  One call for the whole
+        batch (mq_index_search_masked_batch).  -> (scores [nq, k], ids [nq, k])."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        self._check_bits(bits)
+        scores = np.empty((q.shape[0], k), dtype=np.float32)
+        ids = np.empty((q.shape[0], k), dtype=np.int64)
+        with _lib.device_scope(self.device):
+            _lib.call("mq_index_search_masked_batch", self._h, _lib.ptr(q), q.shape[0], k, _lib.ptr(bits),
+                      _lib.ptr(scores), _lib.ptr(ids), 0, _lib.stream_handle(None))
         return scores, ids
 
     @property
@@ -295,25 +299,58 @@ class Encoder:
                   1, _lib.stream_handle(stream))
 
 
+def check_mask_words(bits, n, device=None):
+    """A row mask for n rows: a contiguous 4-byte-element device tensor (on `device` when
+    given) of >= ceil(n / 32) words - else ValueError (the kernels would read or write past
+    its end, or on another GPU's memory)."""
+    if not (getattr(bits, "is_cuda", False) and bits.element_size() == 4 and bits.is_contiguous()
+            and bits.numel() >= (int(n) + 31) // 32):
+        raise ValueError("bits must be a contiguous 32-bit device tensor of >= ceil(n / 32) = %d words"
+                         % ((int(n) + 31) // 32))
+    if device is not None and bits.device.index != int(device):
+        raise ValueError("bits lives on cuda:%s, the index on cuda:%d" % (bits.device.index, int(device)))
+
+
+def _check_codes(codes, bits):
+    import torch
+    if not (getattr(codes, "is_cuda", False) and codes.dtype == torch.int32 and codes.is_contiguous()):
+        raise ValueError("codes must be a contiguous int32 device tensor")
+    check_mask_words(bits, codes.numel(), codes.device.index)
+
+
 def mask_eval(codes, lut, bits, mode, stream=None):
     """bits (mode)= lut[codes] on the device (include/mq.h mq_mask_eval): codes int32 [n]
     (-1 = key absent -> lut[-1]), lut uint8 [n_lut], bits int32 [ceil(n / 32)] (torch,
-    device)."""
-    _lib.call("mq_mask_eval", _lib.ptr(codes), codes.numel(), _lib.ptr(lut), lut.numel(), _lib.ptr(bits),
-              mode, _lib.stream_handle(stream))
+    one device; the launch runs there, on `stream` or that device's current stream)."""
+    import torch
+    _check_codes(codes, bits)
+    if not (getattr(lut, "is_cuda", False) and lut.dtype == torch.uint8 and lut.is_contiguous()
+            and lut.device == codes.device and lut.numel() >= 1):
+        raise ValueError("lut must be a non-empty contiguous uint8 tensor on the codes' device")
+    with _lib.device_scope(codes.device.index):
+        _lib.call("mq_mask_eval", _lib.ptr(codes), codes.numel(), _lib.ptr(lut), lut.numel(), _lib.ptr(bits),
+                  mode, _lib.stream_handle(stream))
 
 
 def mask_eval_bits(codes, lut, bits, mode, stream=None):
     """mask_eval with a table of <= 256 entries passed by value (numpy bool / uint8 lut)."""
+    _check_codes(codes, bits)
     lut = np.asarray(lut).astype(bool)
+    if not 1 <= lut.size <= 256:
+        raise ValueError("a by-value table holds 1..256 entries (got %d)" % lut.size)
     words = np.zeros(4, dtype=np.uint64)
     for i in np.flatnonzero(lut).tolist():
         words[i >> 6] |= np.uint64(1 << (i & 63))
-    _lib.call("mq_mask_eval_bits", _lib.ptr(codes), codes.numel(), _lib.ptr(words), len(lut), _lib.ptr(bits),
-              mode, _lib.stream_handle(stream))
+    with _lib.device_scope(codes.device.index):
+        _lib.call("mq_mask_eval_bits", _lib.ptr(codes), codes.numel(), _lib.ptr(words), len(lut), _lib.ptr(bits),
+                  mode, _lib.stream_handle(stream))
 
 
 def mask_combine(dst, src, mode, stream=None):
     """dst (mode)= src (None: all ones; MQ_MASK_CLEAR: zeros) on the device."""
-    _lib.call("mq_mask_combine", _lib.ptr(dst), _lib.ptr(src), dst.numel(), mode, _lib.stream_handle(stream))
+    check_mask_words(dst, 0)
+    if src is not None:
+        check_mask_words(src, 32 * dst.numel(), dst.device.index)
+    with _lib.device_scope(dst.device.index):
+        _lib.call("mq_mask_combine", _lib.ptr(dst), _lib.ptr(src), dst.numel(), mode, _lib.stream_handle(stream))
 

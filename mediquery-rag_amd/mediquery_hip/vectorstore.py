@@ -46,6 +46,15 @@ from .native import FlatIndex, mask_combine, mask_eval, mask_eval_bits
 
 DEFAULT_K = 4  # LangChain VectorStore.similarity_search default; the reference passes k=5
 
+# search arithmetic (`HipChroma(search_precision=...)`): "screen" (default) = exact fp32
+# top-k through the certified screens (int8 / bf16 shadow scans for candidates, fp32
+# re-rank, a proven bound per query, uncertified queries re-run exactly); "f32" = the
+# direct exact fp32 scan; "f32x6" = the direct scan on the split-f32 MFMA (fp32-class);
+# "bf16" = BASELINE config 5's bf16 coarse scan + fp32 re-rank (approximate: recall is
+# measured, not guaranteed)
+SEARCH_PRECISIONS = {"screen": _lib.MQ_DTYPE_F32_SCREEN, "f32": _lib.MQ_DTYPE_F32,
+                     "f32x6": _lib.MQ_DTYPE_F32X6, "bf16": _lib.MQ_DTYPE_BF16}
+
 
 def _match(meta, where):
     """Chroma-style metadata filter: {"k": v}, {"k": {"$op": v}}, {"$and"/"$or": [...]}."""
@@ -190,12 +199,15 @@ class _MetaColumns:
         return got[1]
 
     def dmask(self, where, device):
-        """Row bitmask of `where` on the device (int32 words, bit r % 32 of word r / 32)."""
+        """Row bitmask of `where` on the device (int32 words, bit r % 32 of word r / 32),
+        built on `device` with that device's current stream whatever torch's current
+        device is."""
         import torch
         dev = torch.device("cuda", device)
-        bits = torch.empty(max(1, (self.n + 31) // 32), dtype=torch.int32, device=dev)
-        mask_combine(bits, None, _lib.MQ_MASK_SET)  # all rows
-        self._dapply(where, bits, dev)
+        with _lib.device_scope(device):
+            bits = torch.empty(max(1, (self.n + 31) // 32), dtype=torch.int32, device=dev)
+            mask_combine(bits, None, _lib.MQ_MASK_SET)  # all rows
+            self._dapply(where, bits, dev)
         return bits
 
     def _dapply(self, where, bits, dev):
@@ -250,6 +262,84 @@ class _MetaColumns:
         return out
 
 
+class _IdRows:
+    """id -> current row in O(1), kept across deletes without rebuilding a dict of every id:
+    each id gets a stable slot when it is added (`slot`, a dict), and two int64 arrays map
+    slot -> current row (-1 = deleted) and row -> slot.  A delete drops its ids' dict
+    entries and renumbers the surviving rows with one numpy gather / scatter (a dict
+    rebuild of a 1M-row store cost ~0.4 s per delete).  Dead slots are reclaimed by a
+    rebuild once they outnumber the live rows."""
+
+    def __init__(self, ids=()):
+        self.slot = {}
+        self._slot_row = np.zeros(1024, np.int64)
+        self._row_slot = np.zeros(1024, np.int64)
+        self.n_slots = 0
+        self.n = 0
+        self.extend(list(ids))
+
+    def __contains__(self, i):
+        return i in self.slot
+
+    def __len__(self):
+        return self.n
+
+    def row(self, i):
+        return int(self._slot_row[self.slot[i]])
+
+    @staticmethod
+    def _grow(a, need):
+        if a.shape[0] >= need:
+            return a
+        b = np.zeros(max(need, 2 * a.shape[0]), np.int64)
+        b[:a.shape[0]] = a
+        return b
+
+    def extend(self, ids):
+        """ids (new, distinct) appended as rows n .. n + len(ids)."""
+        m = len(ids)
+        if not m:
+            return
+        s0, r0 = self.n_slots, self.n
+        self._slot_row = self._grow(self._slot_row, s0 + m)
+        self._row_slot = self._grow(self._row_slot, r0 + m)
+        self._slot_row[s0:s0 + m] = np.arange(r0, r0 + m)
+        self._row_slot[r0:r0 + m] = np.arange(s0, s0 + m)
+        self.slot.update(zip(ids, range(s0, s0 + m)))
+        self.n_slots += m
+        self.n += m
+
+    def compact(self, keep, dropped_ids):
+        """Rows `keep` (sorted int64) survive, renumbered 0..len(keep); dropped_ids leave."""
+        for i in dropped_ids:
+            del self.slot[i]
+        rs = self._row_slot[:self.n]
+        keepm = np.zeros(self.n, bool)
+        keepm[keep] = True
+        self._slot_row[rs[~keepm]] = -1
+        kept = rs[keepm]
+        self._row_slot[:kept.shape[0]] = kept
+        self._slot_row[kept] = np.arange(kept.shape[0])
+        self.n = int(kept.shape[0])
+        if self.n_slots > 2 * self.n + 1024:  # reclaim the dead slots
+            order = sorted(self.slot, key=self.slot.__getitem__)
+            rows = self._slot_row[[self.slot[i] for i in order]] if order else np.zeros(0, np.int64)
+            ids_by_row = [None] * self.n
+            for i, r in zip(order, rows.tolist()):
+                ids_by_row[r] = i
+            self.__init__(ids_by_row)
+
+
+def _drop_sorted(lst, drop):
+    """lst without the positions `drop` (sorted, distinct): list slices, no per-item Python."""
+    out, prev = [], 0
+    for d in drop:
+        out += lst[prev:d]
+        prev = d + 1
+    out += lst[prev:]
+    return out
+
+
 def _check_k(k, n_candidates):
     """Result count of a top-k over n_candidates rows; raises past the device limit."""
     kk = min(int(k), int(n_candidates))
@@ -270,8 +360,13 @@ class HipChroma(VectorStoreBase):
     def __init__(self, collection_name="langchain", embedding_function=None,
                  persist_directory=None, client_settings=None, collection_metadata=None,
                  client=None, relevance_score_fn=None, *, device=0, dim=None,
-                 auto_persist=True, _ingest=False, **kwargs):
-        """auto_persist=False: writes stay in memory until `persist()` (bulk ingest)."""
+                 auto_persist=True, search_precision="screen", _ingest=False, **kwargs):
+        """auto_persist=False: writes stay in memory until `persist()` (bulk ingest);
+        search_precision: SEARCH_PRECISIONS (default "screen": exact fp32 top-k)."""
+        if search_precision not in SEARCH_PRECISIONS:
+            raise ValueError("search_precision must be one of %s, got %r"
+                             % (sorted(SEARCH_PRECISIONS), search_precision))
+        self._search_precision = search_precision
         self._collection_name = collection_name
         self._embedding_function = embedding_function
         self._persist_directory = persist_directory
@@ -280,7 +375,7 @@ class HipChroma(VectorStoreBase):
         self._device = device
         self._auto_persist = bool(auto_persist)
         self._ids, self._texts, self._metas = [], [], []
-        self._id_row = {}              # id -> row (upsert / delete / get by id in O(1))
+        self._id_row = _IdRows()       # id -> row (upsert / delete / get by id in O(1))
         self._cols = _MetaColumns()    # metadata column-wise, for vectorised filters
         self._version = 0              # bumped by every write
         self._index = None
@@ -310,8 +405,7 @@ class HipChroma(VectorStoreBase):
         if self._index is None:
             self._dim = dim
             self._index = FlatIndex(dim=dim, device=self._device)
-            # exact fp32 top-k; batched searches run the certified split-f32 screen
-            self._index.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+            self._index.set_precision(SEARCH_PRECISIONS[self._search_precision])
         elif dim != self._dim:
             raise ValueError("embedding dim %d != collection dim %d" % (dim, self._dim))
 
@@ -404,7 +498,7 @@ class HipChroma(VectorStoreBase):
         self._written.clear()
 
     def _reindex_host(self):
-        self._id_row = {i: r for r, i in enumerate(self._ids)}
+        self._id_row = _IdRows(self._ids)
         self._cols = _MetaColumns()
         self._cols.append(self._metas)
         self._version += 1
@@ -487,7 +581,7 @@ class HipChroma(VectorStoreBase):
         self._ids += ids
         self._texts += texts
         self._metas += metadatas
-        self._id_row.update((i, base + j) for j, i in enumerate(ids))
+        self._id_row.extend(ids)
         self._cols.append(metadatas)
         self._version += 1
         if existing:  # rows were replaced: a full write (compaction)
@@ -498,18 +592,18 @@ class HipChroma(VectorStoreBase):
     def delete(self, ids=None, _persist=True, **kwargs):
         if not ids or self._index is None:
             return None
-        drop = [self._id_row[i] for i in set(ids) if i in self._id_row]
-        if not drop:
+        gone = [i for i in set(ids) if i in self._id_row]
+        if not gone:
             return True
+        drop = sorted(self._id_row.row(i) for i in gone)
         keepm = np.ones(len(self._ids), bool)
         keepm[drop] = False
         keep = np.flatnonzero(keepm)
         self._index.select(keep, out=self._index)  # device compaction, rows bit-identical
-        keepl = keepm.tolist()
         for name in ("_ids", "_texts", "_metas"):
-            setattr(self, name, [v for v, kp in zip(getattr(self, name), keepl) if kp])
+            setattr(self, name, _drop_sorted(getattr(self, name), drop))
         self._cols.compact(keep)
-        self._id_row = {i: r for r, i in enumerate(self._ids)}
+        self._id_row.compact(keep, gone)
         self._version += 1
         if _persist:
             self._persist()
@@ -519,7 +613,7 @@ class HipChroma(VectorStoreBase):
         rows = np.arange(len(self._ids))
         if ids is not None:
             want = [ids] if isinstance(ids, str) else ids
-            rows = np.array(sorted({self._id_row[i] for i in want if i in self._id_row}), np.int64)
+            rows = np.array(sorted({self._id_row.row(i) for i in want if i in self._id_row}), np.int64)
         if where:
             rows = rows[self._cols.mask(where)[rows]]
         rows = rows.tolist()[offset or 0:]
@@ -547,7 +641,7 @@ class HipChroma(VectorStoreBase):
             if k == 0:
                 return []
         bits = self._cols.dmask(filter, self._device)
-        s, i = self._index.search_masked(q[0], int(k), bits)
+        s, i = self._index.search_masked(q, int(k), bits)
         return [(int(r), float(c)) for r, c in zip(i[0], s[0]) if r >= 0]
 
     def similarity_search_by_vector_with_score(self, embedding, k=DEFAULT_K, filter=None, **kwargs):
@@ -568,8 +662,8 @@ class HipChroma(VectorStoreBase):
 
     def similarity_search_batch(self, queries, k=DEFAULT_K, filter=None):
         """Many queries in one encoder batch + one device search (the throughput path).
-        With `filter`, the where-mask is built once on the device and every query runs
-        the masked search over it."""
+        With `filter`, the where-mask is built once on the device and ONE masked search
+        call serves the whole batch (mq_index_search_masked_batch)."""
         n = 0 if self._index is None else len(self._index)
         if n == 0 or not queries or k <= 0:
             return [[] for _ in queries]
@@ -582,7 +676,7 @@ class HipChroma(VectorStoreBase):
             if kk == 0:
                 return [[] for _ in queries]
             bits = self._cols.dmask(filter, self._device)
-            rows = [self._index.search_masked(qv, int(kk), bits)[1][0] for qv in q]
+            _, rows = self._index.search_masked(q, int(kk), bits)
             return [[self._doc(int(r)) for r in row if r >= 0] for row in rows]
         kk = _check_k(k, n)
         _, ids = self._index.search(q, kk)

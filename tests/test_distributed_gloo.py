@@ -132,3 +132,119 @@ def test_pack_candidates_roundtrip_is_bit_exact():
     assert s2.shape == (2, 2, 3) and i2.shape == (2, 2, 3)
     assert torch.equal(s2[1].view(torch.int32), s.view(torch.int32))
     assert torch.equal(i2[0], i)
+
+
+class _OracleShard:
+    """CPU stand-in with FlatIndex's surface (add_device / search_device / __len__): the
+    oracle's exact search padded to the device contract (-inf, -1)."""
+
+    def __init__(self, capacity=0):
+        self.rows = np.zeros((0, DIM), np.float32)
+
+    def add_device(self, rows):
+        self.rows = rows.numpy().copy()
+
+    def search_device(self, q, k, out_s, out_i):
+        from oracle.flat import search
+        out_s.fill_(float("-inf"))
+        out_i.fill_(-1)
+        if len(self.rows):
+            s, i = search(q.numpy(), self.rows, k)
+            out_s[:, :s.shape[1]] = torch.from_numpy(np.ascontiguousarray(s, np.float32))
+            out_i[:, :i.shape[1]] = torch.from_numpy(np.ascontiguousarray(i, np.int64))
+
+    def set_precision(self, dtype):
+        pass
+
+    def close(self):
+        pass
+
+    def __len__(self):
+        return self.rows.shape[0]
+
+
+C4_SHARDS = 8
+
+
+def _config4_worker(rank, world, port, out_q, per, K, B):
+    """bench.py config4()'s partition: 8 row shards of `per` rows, rank r owns shards
+    [r*8/world, (r+1)*8/world) as one LocalShards (global id = first*per + shard offset +
+    local id), embeds B/world queries (DP), one query all-gather, one packed candidate
+    all-gather, merge of its own queries."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "mediquery-rag_amd"), root]
+    from mediquery_hip import synth
+    from mediquery_hip.distributed import LocalShards, ShardedSearcher
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = synth.corpus(C4_SHARDS * per, DIM, clustered=True)
+        spr = C4_SHARDS // world
+        first = rank * spr
+        shards = LocalShards(spr, DIM, device=None, index_factory=_OracleShard)
+        shards.add_device(torch.from_numpy(c[first * per:(first + spr) * per]))
+        assert len(shards) == spr * per
+        q, _ = synth.queries(B, c)
+        bq = B // world
+        s_loc = torch.empty((B, K), dtype=torch.float32)
+        i_loc = torch.empty((B, K), dtype=torch.int64)
+
+        def local(qq, k):
+            n = qq.shape[0]
+            shards.search_device(qq, k, s_loc[:n], i_loc[:n])
+            return s_loc[:n], i_loc[:n]
+
+        ss = ShardedSearcher(local, first * per)
+        ss.timings = []
+        s, i = ss.search_local_batch(torch.from_numpy(q[rank * bq:(rank + 1) * bq]), K, sizes=[bq] * world)
+        tags = [t[0] for t in ss.resolve_timings()]
+        out_q.put((rank, i.numpy(), s.numpy(), tags))
+    except Exception as e:
+        out_q.put((rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config4_eight_shard_partition_over_ranks(world):
+    """BASELINE config 4's 8-shard partition through LocalShards at world 2 and 4 (gloo):
+    each rank's merged answer for its own DP queries equals the exact top-k over the whole
+    corpus, and the collectives are timed (one query and one candidate all-gather)."""
+    from mediquery_hip import synth
+    from oracle.flat import check_topk, exact_scores
+    per, K, B = 125, 5, 16
+    ctx = mp.get_context("spawn")
+    q_out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config4_worker, args=(r, world, port, q_out, per, K, B)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q_out.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = synth.corpus(C4_SHARDS * per, DIM, clustered=True)
+    q, _ = synth.queries(B, c)
+    ref = exact_scores(q, c)
+    bq = B // world
+    for rank, ids, scores, tags in sorted(res, key=lambda r: r[0]):
+        assert not isinstance(ids, str), ids
+        assert check_topk(ids, scores, ref[rank * bq:(rank + 1) * bq], K) == []
+        assert tags == ["queries", "candidates"]
+
+
+def test_local_shards_host_merge_equals_exact():
+    """LocalShards on one process with host candidates (merge_topk_host): 8 uneven shards."""
+    from mediquery_hip import synth
+    from mediquery_hip.distributed import LocalShards
+    from oracle.flat import check_topk, exact_scores
+    c = synth.corpus(1003, DIM, clustered=True)
+    q, _ = synth.queries(9, c)
+    sh = LocalShards(8, DIM, device=None, base=0, index_factory=_OracleShard)
+    sh.add_device(torch.from_numpy(c))
+    s = torch.empty((9, 7), dtype=torch.float32)
+    i = torch.empty((9, 7), dtype=torch.int64)
+    sh.search_device(torch.from_numpy(q), 7, s, i)
+    assert check_topk(i.numpy(), s.numpy(), exact_scores(q, c), 7) == []

@@ -117,7 +117,7 @@ def test_wide_filters_certify_on_the_int8_screen(big_store):
 
 
 def test_batch_search_with_filter_matches_single(require_gpu, big_store):
-    """similarity_search_batch(filter=) (one device mask, one masked search per query)
+    """similarity_search_batch(filter=) (one device mask, one batched masked search call)
     returns what the single-query path returns, query by query."""
     store, rows64, metas = big_store
 
@@ -155,3 +155,100 @@ def test_mask_by_value_table_past_64_entries(require_gpu):
         got = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
         assert np.array_equal(got, want), n_lut
 
+
+
+def _rows_fp64_topk(rows64, allowed, Q, k):
+    import torch
+    al = torch.as_tensor(allowed, device=rows64.device)
+    ref = (torch.as_tensor(Q, dtype=torch.float64, device=rows64.device) @ rows64[al].T).cpu().numpy()
+    return ref
+
+
+@pytest.mark.parametrize("where,k", [
+    ({"src": 3}, 5),                                   # 1/7 of the rows: masked K9t + certificate
+    ({"$or": [{"src": 1}, {"year": {"$gte": 40}}]}, 16),
+    ({"src": 3}, 20),                                  # k > 16: the masked streaming exact scan
+    ({"rare": "yes"}, 5),                              # two rows: fewer than k, padded
+])
+def test_batched_filtered_search_256_equals_fp64(big_store, where, k):
+    """256 queries with one filter in ONE masked call (the bf16 threshold
+    scan with the row mask, fp32 re-rank, certificate; the masked streaming exact scan for
+    what it does not certify and for k > 16): every query's answer against float64 over the
+    allowed rows, tie-group aware."""
+    import torch
+    store, rows64, metas = big_store
+    allowed = np.array([r for r, m in enumerate(metas) if _match(m, where)], dtype=np.int64)
+    rng = np.random.default_rng(77)
+    src = rng.integers(0, len(metas), 256)
+    Q = rows64[torch.as_tensor(src, device=rows64.device)].float().cpu().numpy()
+    Q += 0.02 * rng.standard_normal(Q.shape).astype(np.float32)
+    bits = store._cols.dmask(where, store._device)
+    s, i = store._index.search_masked(Q, k, bits)
+    assert s.shape == (256, k) and i.shape == (256, k)
+    kk = min(k, len(allowed))
+    assert (i[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
+    ref = _rows_fp64_topk(rows64, allowed, Q, k)
+    pos = {int(r): j for j, r in enumerate(allowed)}
+    for qi in range(256):
+        order = np.lexsort((allowed, -ref[qi]))
+        fails = check_topk(i[qi:qi + 1, :kk], s[qi:qi + 1, :kk], None, kk,
+                           ref_top=(ref[qi][order][None, :kk + 1], allowed[order][None, :kk + 1]),
+                           n_rows=len(rows64),
+                           ref_lookup=lambda b, rr, qi=qi: ref[qi][[pos[int(x)] for x in rr]]
+                           if all(int(x) in pos for x in rr) else np.full(len(rr), -np.inf))
+        assert fails == [], (where, qi, fails[:3])
+
+
+def test_batched_filtered_search_cost_vs_unfiltered(big_store):
+    """The 256-query filtered batch costs about what the unfiltered batch costs (the mask is
+    1/6144 of the scan's bytes): measured and printed; asserted within 3x (VERDICT r5 #9's
+    target is 2x, reported by tools/filter_latency.py on a quiet box)."""
+    import time
+    import torch
+    store, rows64, metas = big_store
+    rng = np.random.default_rng(5)
+    Q = rows64[torch.as_tensor(rng.integers(0, len(metas), 256), device=rows64.device)].float().cpu().numpy()
+    where = {"src": {"$ne": 3}}
+    bits = store._cols.dmask(where, store._device)
+    ix = store._index
+    for _ in range(2):
+        ix.search(Q, 5)
+        ix.search_masked(Q, 5, bits)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ix.search(Q, 5)
+    t_plain = (time.perf_counter() - t0) / 5
+    g0 = ix.masked_gathers
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ix.search_masked(Q, 5, bits)
+    t_mask = (time.perf_counter() - t0) / 5
+    print("batch256_unfiltered_ms %.3f filtered_ms %.3f ratio %.2f uncertified %d"
+          % (t_plain * 1e3, t_mask * 1e3, t_mask / t_plain, ix.masked_gathers - g0))
+    assert t_mask <= 3.0 * t_plain, (t_mask, t_plain)
+
+
+def test_selective_filter_fewer_than_k_rows_certifies(big_store):
+    """a filter admitting fewer than k rows (n >= 65536) is answered by the int8
+    screen itself (tau = -inf: every allowed row survived) - no uncertified fallback."""
+    store, rows64, metas = big_store
+    g0 = store._index.masked_gathers
+    for r in (123456, 654321, 7):
+        q = rows64[r].float().cpu().numpy()
+        got = store._search_rows(q, 5, {"rare": "yes"})
+        assert sorted(x for x, _ in got) == [123456, 654321]
+    assert store._index.masked_gathers == g0
+
+
+def test_mask_on_another_device_or_short_is_rejected(big_store):
+    """The masked search checks the mask's device, width and length before any kernel runs."""
+    import torch
+    store, rows64, metas = big_store
+    q = rows64[0].float().cpu().numpy()
+    short = torch.zeros(10, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(ValueError, match="ceil"):
+        store._index.search_masked(q, 5, short)
+    with pytest.raises(ValueError):
+        store._index.search_masked(q, 5, torch.zeros((len(metas) + 31) // 32, dtype=torch.int64, device="cuda:0"))
+    with pytest.raises(ValueError):
+        store._index.search_masked(q, 5, torch.zeros((len(metas) + 31) // 32, dtype=torch.int32))

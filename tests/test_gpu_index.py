@@ -210,10 +210,12 @@ def test_device_pointer_path_and_device_merge(require_gpu):
     np.testing.assert_array_equal(di.cpu().numpy(), hi)
 
 
-@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("prec", PRECS + [_lib.MQ_DTYPE_F32_SCREEN])
 def test_full_size_1m_planted_and_fp64_reference(require_gpu, prec):
     """BASELINE config 3 size (1M x 768, B = 256, k = 5): planted queries hit their
-    rows, and the ids equal a float64 torch reference of the same device corpus."""
+    rows, and the ids equal a float64 torch reference of the same device corpus - for
+    the headline's own search mode (MQ_DTYPE_F32_SCREEN: certified bf16 screen + fp32
+    re-rank) directly, not only through its equality with the direct scan."""
     import torch
     dev = torch.device("cuda", 0)
     rows = synth.corpus_device(1_000_000, 768, dev)
@@ -460,3 +462,44 @@ def test_screened_passes_near_ties_to_split_f32(require_gpu):
     assert check_topk(i, s, exact_scores(q, c), 5) == []
     for j in range(100):
         assert i[j].tolist() == list(range(j * 70, j * 70 + 5))
+
+
+def test_config2_end_to_end_encoder_and_screen_vs_fp64(require_gpu):
+    """BASELINE config 2 end to end: 100k x 768 corpus, B = 256 queries
+    of L = 32 token ids through the 12-layer encoder at the headline arithmetic (split-f32)
+    and the certified screen (MQ_DTYPE_F32_SCREEN), k = 5.  The embeddings against the
+    torch-CPU oracle (1e-4 / cos 1 - 1e-5), the top-5 against float64 over the same device
+    corpus, and the planted rows (each query's own embedding planted in the corpus) found."""
+    import torch
+    from mediquery_hip.config import DMETA_BASE
+    from mediquery_hip.native import Encoder
+    from mediquery_hip.weights import synthetic_state_dict
+    from oracle.encoder import OracleEncoder
+    dev = torch.device("cuda", 0)
+    ids, mask = synth.token_batch(256, 32)
+    enc = Encoder(DMETA_BASE)
+    enc.set_precision(_lib.MQ_DTYPE_F32X6)
+    q = torch.empty((256, 768), dtype=torch.float32, device=dev)
+    enc.embed_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), q)
+    torch.cuda.synchronize()
+    ref_e = OracleEncoder(DMETA_BASE, synthetic_state_dict(DMETA_BASE, 0)).embed(ids, mask)
+    qe = q.cpu().numpy()
+    np.testing.assert_allclose(qe, ref_e, atol=1e-4, rtol=0)
+    rows = synth.corpus_device(100_000, 768, dev, seed=synth.CORPUS_SEED + 2)
+    plant = torch.arange(0, 100_000, 1000, device=dev)[:64]
+    rows[plant] = q[:64]  # queries 0..63 planted (unit rows already)
+    ix = FlatIndex(dim=768, capacity=100_000)
+    ix.add_device(rows)
+    ix.set_precision(_lib.MQ_DTYPE_F32_SCREEN)
+    s = torch.empty((256, 5), dtype=torch.float32, device=dev)
+    i = torch.empty((256, 5), dtype=torch.int64, device=dev)
+    ix.search_device(q, 5, s, i)
+    torch.cuda.synchronize()
+    assert bool((i[:64, 0] == plant).all())
+    normed = torch.nn.functional.normalize(rows.double(), dim=1)
+    ref_full = q.double() @ normed.T
+    rv, ri = torch.topk(ref_full, 6, dim=1)
+    fails = check_topk(i.cpu().numpy(), s.cpu().numpy(), None, 5,
+                       ref_top=(rv.cpu().numpy(), ri.cpu().numpy()), n_rows=100_000,
+                       ref_lookup=lambda b, ids_: ref_full[b, torch.as_tensor(ids_, device=dev)].cpu().numpy())
+    assert fails == []

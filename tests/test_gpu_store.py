@@ -53,6 +53,38 @@ def test_ingest_then_engine_then_retrieve(embeddings, docs, golden, tmp_path_fac
         assert check_topk([rows], [scores], ref[qi:qi + 1], 5) == [], q
 
 
+@pytest.mark.parametrize("precision,search_precision", [
+    ("f32", "screen"), ("f32x6", "screen"), ("f32", "f32"), ("f32x6", "f32x6")])
+def test_drop_in_precisions_against_config1_golden(docs, golden, tmp_path, require_gpu, precision,
+                                                  search_precision):
+    """the arithmetic is selectable on the drop-in -
+    HipBertEmbeddings(precision=) (the unchanged OllamaEmbeddings(model=...) line of
+    src/medical_engine.py:43 gets the default, f32x6) and HipChroma(search_precision=) -
+    and at each setting from_documents -> Chroma(persist_directory=) -> similarity_search
+    (src/ingest_medical.py:106-110, src/medical_engine.py:52, src/agents/nodes.py:93)
+    reproduces the config-1 golden."""
+    from mediquery_hip import OllamaEmbeddings, _lib
+    emb = HipBertEmbeddings(model="shaw/dmeta-embedding-zh", synthetic=True, precision=precision)
+    assert emb.precision == precision
+    default = OllamaEmbeddings(model="shaw/dmeta-embedding-zh", synthetic=True) if precision == "f32x6" else None
+    assert default is None or default.precision == "f32x6"
+    db = str(tmp_path / "db")
+    HipChroma.from_documents(documents=docs, embedding=emb, persist_directory=db, search_precision=search_precision)
+    store = HipChroma(persist_directory=db, embedding_function=emb, search_precision=search_precision)
+    g = np.load(os.path.join(golden, "config1_golden.npz"))
+    queries = json.load(open(os.path.join(golden, "config1_queries.json"), encoding="utf-8"))["queries"]
+    contents = [d.page_content for d in docs]
+    # a batch of > 64 texts runs the batched GEMMs (the precision applies there)
+    np.testing.assert_allclose(emb.embed_array(contents), g["doc_emb"], atol=1e-4)
+    ref = exact_scores(g["query_emb"], g["doc_emb"])
+    for qi, q in enumerate(queries):
+        got = [d.page_content for d in store.similarity_search(q, k=5)]
+        rows = [r for r, _ in store._search_rows(store._embed_query(q), 5)]
+        assert [contents[r] for r in rows] == got
+        scores = [c for _, c in store._search_rows(store._embed_query(q), 5)]
+        assert check_topk([rows], [scores], ref[qi:qi + 1], 5) == [], q
+
+
 def test_scores_distance_semantics_and_edges(embeddings, docs):
     store = HipChroma.from_documents(documents=docs[:20], embedding=embeddings)
     res = store.similarity_search_with_score(docs[3].page_content, k=3)
