@@ -752,12 +752,40 @@ __device__ __forceinline__ floatx4 load_w(__amdgpu_buffer_rsrc_t w, int byte_off
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const float* W) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0x7fffffff, 0x00020000);
 }
+// Fragment image ("frag16") of a [R][C] fp32 matrix for the few-row kernels: per 16-row x
+// 16-column block (block (rb, cb), cb fastest) 1 KB in the lane order of one
+// v_mfma_f32_16x16x4_f32 operand load - lane l = c + 16 kq holds the float4 at row
+// 16 rb + c, columns 16 cb + 4 kq .. + 3.  One wave-instruction then moves 1 KB of whole
+// lines, where the row-major operand loads moved 16 rows x 64 B (16 half lines) each;
+// profiles/r6/engine_probe.jsonl: 5.76 -> 3.37 us for FFN-down's per-workgroup bytes.
+// The weights are imaged once at load (mq_encoder_load_weights); FFN-up writes its output
+// in this layout for FFN-down (FL_O / FL_A).
+// FL_OT (with FL_O): the blocks of the last third of the columns (QKV's V) are stored
+// transposed - the frag16 of V^T - so attention's P V reads V^T fragments whole
+enum RowsFlags { FL_A = 1, FL_O = 2, FL_OT = 4 };  // A in frag16 / output in frag16 (weights always are)
+__device__ __forceinline__ int64_t frag16_offset(int64_t row, int col, int cols) {  // in floats
+  return ((row >> 4) * (cols >> 4) + (col >> 4)) * 256 + ((row & 15) + 16 * ((col & 15) >> 2)) * 4 + (col & 3);
+}
+__global__ __launch_bounds__(256) void frag16_image_kernel(const float* __restrict__ W, int R, int C,
+                                                           floatx4* __restrict__ img) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of the image
+  if (idx >= (int64_t)R * C / 4) return;
+  const int lane = (int)(idx & 63);
+  const int64_t blk = idx >> 6;
+  const int cbs = C >> 4;
+  const int64_t rb = blk / cbs;
+  const int cb = (int)(blk - rb * cbs);
+  img[idx] = *reinterpret_cast<const floatx4*>(W + (rb * 16 + (lane & 15)) * C + cb * 16 + 4 * (lane >> 4));
+}
+
 constexpr int kRT = 16;      // rows = columns per output tile
 constexpr int kRWaves = 16;  // waves per workgroup, one K range each
 constexpr int kRowsMax = 256; // token rows up to which a forward may take this path
 constexpr int kRowsDefault = 64;  // ... and does by default (MQ_ROWS_MAX overrides)
 
-template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT>
+// W is the weights' frag16 image (ldw = the full depth); FL & FL_A: A (no LayerNorm input)
+// in frag16 with lda columns; FL & FL_O: out in frag16 with ldo columns.
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT, int FL = 0>
 __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ A, int lda, int64_t a_plane, int M, const float* __restrict__ lng,
     const float* __restrict__ lnb, float eps, float* __restrict__ ln_out,
@@ -765,6 +793,7 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane,
     const int* __restrict__ ids, int L, int vocab, const float* __restrict__ pos,
     const float* __restrict__ typ, int nt_w) {
+  static_assert(!(LN_IN && (FL & FL_A)), "a LayerNorm input is read row-major");
   constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
   // 16-deep blocks per load batch: all of them while the operands fit the 128 VGPRs of a
   // 1024-thread workgroup (one memory round trip), else batches
@@ -783,7 +812,9 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   const int kb0 = wave * (K / kRWaves);  // this wave's K range
   const int ks = blockIdx.z;  // K split: columns [ks K, (ks + 1) K) of A and W
   const __amdgpu_buffer_rsrc_t wr = w_rsrc(W);
-  const int wo4 = ((n0 + c) * ldw + ks * K + kb0 + 4 * kq) * 4;  // this lane's weight bytes
+  // this lane's weight fragment: block (n0 / 16, (ks K + kb0) / 16 + j) of the image, 1 KB apart
+  const int kblk0 = (ks * K + kb0) >> 4;
+  const int wo4 = (((n0 >> 4) * (ldw >> 4) + kblk0) * 64 + lane) * 16;
 
   KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 0);
   floatx4 wv[CH], av[RT][CH];
@@ -792,13 +823,19 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   // fragment: the launch streams W once.
 #pragma unroll
   for (int j = 0; j < CH; ++j)
-    wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : load_w(wr, wo4 + 64 * j, nt_w);
+    wv[j] = (MQ_ROWS_DBG & 1) ? floatx4{1e-3f, 1e-3f, 1e-3f, 1e-3f} : load_w(wr, wo4 + 1024 * j, nt_w);
   // Everything else this launch reads from memory goes out now too, under the weight
   // loads: the epilogue's bias / residual element (thread t < 256 RT finishes element
   // t % 256 of row tile t / 256) and the LayerNorm's gamma / beta.  Loaded where they are
   // used, each would add a dependent memory round trip to the launch's critical path
-  // (after the partial-tile reduction, after the row statistics).
-  const int et = threadIdx.x, ert = et / (kRT * kRT), ee = et % (kRT * kRT);
+  // (after the partial-tile reduction, after the row statistics).  FL_O: thread t's element
+  // is position t % 256 of the tile's frag16 block (lane (t % 256) / 4), so each wave
+  // stores 256 contiguous bytes.
+  const int et = threadIdx.x, ert = et / (kRT * kRT), ep = et % (kRT * kRT);
+  const bool vt = (FL & FL_OT) && n0 >= 2 * (ldo / 3);  // a V block of QKV, stored as V^T
+  const int ee = !(FL & FL_O) ? ep
+                 : vt ? ((4 * (ep >> 6) + (ep & 3)) * kRT + ((ep >> 2) & 15))
+                      : (((ep >> 2) & 15) * kRT + 4 * (ep >> 6) + (ep & 3));  // [row][col] in the tile
   const int erow = r0 + ert * kRT + ee / kRT, ecol = n0 + ee % kRT;
   float ebias = 0.f, eres = 0.f;
   if (ert < RT && ks == 0 && erow < M) {
@@ -884,18 +921,25 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   for (int b = 0; b < NB; b += CH) {
     if (b > 0) {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) wv[j] = load_w(wr, wo4 + 64 * (b + j), nt_w);
+      for (int j = 0; j < CH; ++j) wv[j] = load_w(wr, wo4 + 1024 * (b + j), nt_w);
     }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const float* arow = A + (int64_t)min(r0 + rt * kRT + c, M - 1) * lda + ks * K + kb0 + 4 * kq;
+      // frag16 A: row block (r0 / 16 + rt) (rows past M in the last block are never
+      // written; they only feed output rows past M, which are not stored)
+      const floatx4* afr = reinterpret_cast<const floatx4*>(A) +
+                           ((int64_t)((r0 >> 4) + rt) * (lda >> 4) + kblk0) * 64 + lane;
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         if (LN_IN)
           av[rt][j] = *reinterpret_cast<const floatx4*>(&arows[(rt * kRT + c) * AS + kb0 + 16 * (b + j) + 4 * kq]);
+        else if (MQ_ROWS_DBG & 2)
+          av[rt][j] = floatx4{0.1f, 0.2f, 0.3f, 0.4f};
+        else if (FL & FL_A)
+          av[rt][j] = afr[(b + j) * 64];
         else
-          av[rt][j] = (MQ_ROWS_DBG & 2) ? floatx4{0.1f, 0.2f, 0.3f, 0.4f}
-                                        : *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
+          av[rt][j] = *reinterpret_cast<const floatx4*>(arow + 16 * (b + j));
       }
     }
 #pragma unroll
@@ -931,7 +975,10 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     if (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
     if (EPI == EPI_RESID) v += eres;
   }
-  out[ks * o_plane + (int64_t)erow * ldo + ecol] = v;
+  if (FL & FL_O)
+    out[ks * o_plane + (((int64_t)((r0 >> 4) + ert) * (ldo >> 4) + blockIdx.x) << 8) + ep] = v;
+  else
+    out[ks * o_plane + (int64_t)erow * ldo + ecol] = v;
   KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 5);
 }
 
@@ -1317,7 +1364,9 @@ __global__ __launch_bounds__(512) void attention_rows_kernel(const float* __rest
 // b = r / rps (rps = L, or 1 for the CLS-only last layer: query 0, compact rows).
 constexpr int kOpCols = 32;  // output columns per workgroup
 
-template <int HG, int NKB>
+// QF: qkv in frag16 with V^T blocks (QKV's FL_O | FL_OT; needs L % 16 == 0, so every
+// sequence starts a 16-row block): Q, K and V^T fragments load as whole 1 KB blocks.
+template <int HG, int NKB, bool QF = false>
 __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
     const float* __restrict__ qkv, const int* __restrict__ mask, int L, int H, int rps, int qtiles,
     float scale, const float* __restrict__ Wo, const float* __restrict__ bo,
@@ -1343,11 +1392,11 @@ __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
   // K quarter kqr); lane (c, g) holds W[n0 + 16 cb + c][k] at k = kqr KQ + 16 j + 4 g + t
   const int cb = w & 1, kqr = w >> 1;
   floatx4 wv[NJ];
-  {
+  {  // Wo's frag16 image: block ((n0 + 16 cb) / 16, (h0 kDh + kqr KQ) / 16 + j)
     const __amdgpu_buffer_rsrc_t wr = w_rsrc(Wo);
-    const int wo4 = ((n0 + cb * 16 + c) * H + h0 * kDh + kqr * KQ + 4 * g) * 4;
+    const int wo4 = ((((n0 >> 4) + cb) * (H >> 4) + ((h0 * kDh + kqr * KQ) >> 4)) * 64 + lane) * 16;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) wv[j] = load_w(wr, wo4 + 64 * j, nt_w);
+    for (int j = 0; j < NJ; ++j) wv[j] = load_w(wr, wo4 + 1024 * j, nt_w);
   }
   // epilogue element of threads < 512: column block et >> 8, row (et & 255) / 16
   const int et = threadIdx.x, ecb = et >> 8, erow_t = (et & 255) >> 4, ecol = n0 + ecb * 16 + (et & 15);
@@ -1367,24 +1416,47 @@ __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
     const int qpos = rps == 1 ? 0 : min(q0 + c, L - 1);
     floatx4 qf[4], kf[NKB][4];
     float vf[NKB][4][4];
-    const float* qs = qkv + (srow0 + qpos) * ld + h * kDh + 4 * g;
+    if constexpr (QF) {
+      // block (row block, column block) of the [rows][3H] frag16 image; lane = (c, g)
+      const floatx4* f4 = reinterpret_cast<const floatx4*>(qkv);
+      const int cbs = ld >> 4;
+      const int64_t rb0 = srow0 >> 4;
+      auto blk = [&](int64_t rb, int cb) { return f4 + (rb * cbs + cb) * 64 + lane; };
+      // (rps == 1: rows c of block 0 - query 0 is row c = 0, the only one stored)
 #pragma unroll
-    for (int sI = 0; sI < 4; ++sI) qf[sI] = *reinterpret_cast<const floatx4*>(qs + 16 * sI);
+      for (int sI = 0; sI < 4; ++sI) qf[sI] = *blk(rb0 + (q0 >> 4), ((h * kDh) >> 4) + sI);
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-      const float* ks = qkv + (srow0 + min(kb * 16 + c, L - 1)) * ld + H + h * kDh + 4 * g;
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-      for (int sI = 0; sI < 4; ++sI) kf[kb][sI] = *reinterpret_cast<const floatx4*>(ks + 16 * sI);
-    }
-    const float* vs = qkv + srow0 * ld + 2 * H + h * kDh + c;
+        for (int sI = 0; sI < 4; ++sI) kf[kb][sI] = *blk(rb0 + kb, ((H + h * kDh) >> 4) + sI);
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int64_t kk = min(kb * 16 + 4 * g + t, L - 1);
+        for (int db = 0; db < 4; ++db) {  // V^T block: (d = 16 db + c, key = 16 kb + 4 g + t)
+          const floatx4 v = *blk(rb0 + kb, ((2 * H + h * kDh) >> 4) + db);
 #pragma unroll
-        for (int db = 0; db < 4; ++db) vf[kb][db][t] = vs[kk * ld + 16 * db];
+          for (int t = 0; t < 4; ++t) vf[kb][db][t] = v[t];
+        }
+    } else {
+      const float* qs = qkv + (srow0 + qpos) * ld + h * kDh + 4 * g;
+#pragma unroll
+      for (int sI = 0; sI < 4; ++sI) qf[sI] = *reinterpret_cast<const floatx4*>(qs + 16 * sI);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        const float* ks = qkv + (srow0 + min(kb * 16 + c, L - 1)) * ld + H + h * kDh + 4 * g;
+#pragma unroll
+        for (int sI = 0; sI < 4; ++sI) kf[kb][sI] = *reinterpret_cast<const floatx4*>(ks + 16 * sI);
       }
+      const float* vs = qkv + srow0 * ld + 2 * H + h * kDh + c;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int64_t kk = min(kb * 16 + 4 * g + t, L - 1);
+#pragma unroll
+          for (int db = 0; db < 4; ++db) vf[kb][db][t] = vs[kk * ld + 16 * db];
+        }
+    }
     const bool kval = lane < L && mask[srow0 + min(lane, L - 1)] != 0;
     const unsigned long long kbits = __ballot(kval);  // bit k: key k usable
 #pragma unroll
@@ -1603,6 +1675,8 @@ struct LayerW {
   // W3 plane images of the four projection weights (gemm_x6p.hpp), built when the split-f32
   // precision is selected; null otherwise
   const unsigned char *wqkv3 = nullptr, *wo3 = nullptr, *w13 = nullptr, *w23 = nullptr;
+  // frag16 images of the same four (the few-row kernels' weight operands)
+  const float *wqkvf = nullptr, *wof = nullptr, *w1f = nullptr, *w2f = nullptr;
 };
 
 int64_t weight_count(const mq_bert_config& c) {
@@ -1805,6 +1879,7 @@ struct mq_encoder {
   std::vector<LayerW> layers;
   Buf x, y, qkv, ctx, ffn, io_out, slab;  // (+ lnst below)
   Buf w3;  // split-f32: every layer's W3 plane images (LayerW::*3 point into it)
+  Buf wfrag;  // every layer's frag16 weight images (LayerW::*f point into it), built at load
   int* io_ids = nullptr;
   int* io_mask = nullptr;
   size_t io_tokens = 0;
@@ -1867,6 +1942,35 @@ int build_w3(mq_encoder* e) {
     one(w.wo, H, H, w.wo3);
     one(w.w1, F, H, w.w13);
     one(w.w2, H, F, w.w23);
+  }
+  MQ_HIP(hipGetLastError());
+  MQ_HIP(hipStreamSynchronize(nullptr));
+  return MQ_OK;
+}
+
+// The frag16 images of every layer's four projection weights (the few-row kernels' layout,
+// rows_gemm_kernel / attn_oproj_rows_kernel; 4 B per weight, 340 MB for BERT-base beside the
+// row-major blob the batched GEMMs read).  Synchronous.
+int build_frag16(mq_encoder* e) {
+  const mq_bert_config& c = e->cfg;
+  const int64_t H = c.hidden, F = c.ffn;
+  const int64_t per = 3 * H * H + H * H + F * H + H * F;
+  DeviceGuard dg(e->device);
+  int rc = e->wfrag.ensure((size_t)(per * (int64_t)e->layers.size()));
+  if (rc) return rc;
+  float* p = e->wfrag.p;
+  for (LayerW& w : e->layers) {
+    auto one = [&](const float* W, int64_t r, int64_t k, const float*& dst) {
+      const int64_t n4 = r * k / 4;
+      hipLaunchKernelGGL(frag16_image_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, nullptr, W, (int)r,
+                         (int)k, reinterpret_cast<floatx4*>(p));
+      dst = p;
+      p += r * k;
+    };
+    one(w.wqkv, 3 * H, H, w.wqkvf);
+    one(w.wo, H, H, w.wof);
+    one(w.w1, F, H, w.w1f);
+    one(w.w2, H, F, w.w2f);
   }
   MQ_HIP(hipGetLastError());
   MQ_HIP(hipStreamSynchronize(nullptr));
@@ -2078,26 +2182,26 @@ struct RowsArgs {
 // FFN-up 10.1 -> 8.6 us at M = 32), unless the normalised rows would not fit LDS (hidden
 // 1024).  The plain GEMMs keep one: with half the workgroups their per-CU bytes, not the
 // chip's, bound them (FFN-down 7.8 -> 10.9 us with two).
-template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT>
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int RT, int FL>
 void launch_rows_rt(const RowsArgs& g, const float* lng, const float* lnb, float eps, float* ln_out,
                     hipStream_t s) {
-  hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN, RT>),
+  hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN, RT, FL>),
                      dim3(g.N / kRT, (g.M + kRT * RT - 1) / (kRT * RT), g.splits), dim3(64 * kRWaves), 0, s,
                      g.A, g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
                      g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ, g.nt_w);
 }
 
-template <int EPI, bool LN_IN, int VPL, int NB, int S_IN>
+template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int FL = 0>
 void launch_rows_nb(const RowsArgs& g, const float* lng, const float* lnb, float eps, float* ln_out,
                     hipStream_t s) {
   constexpr bool two_fit = LN_IN && (size_t)(2 * kRT * (NB * 256 + 4) + kRWaves * 2 * kRT * kRT) * 4 <= 160 * 1024;
   if constexpr (two_fit) {
     if (g.M > kRT) {
-      launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 2>(g, lng, lnb, eps, ln_out, s);
+      launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 2, FL>(g, lng, lnb, eps, ln_out, s);
       return;
     }
   }
-  launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 1>(g, lng, lnb, eps, ln_out, s);
+  launch_rows_rt<EPI, LN_IN, VPL, NB, S_IN, 1, FL>(g, lng, lnb, eps, ln_out, s);
 }
 
 // Per-split depths the few-row kernel is instantiated for (K / 256 blocks per wave).
@@ -2115,41 +2219,41 @@ int rows_splits(int K, int forced = 0) {  // forced: MQ_ENC_OPT_ROWS_SPLITS, use
   return 1;
 }
 
-template <int EPI, int NB>
+template <int EPI, int NB, int FL>
 void launch_rows_plain(const RowsArgs& g, hipStream_t s) {
-  launch_rows_nb<EPI, false, 1, NB, 1>(g, nullptr, nullptr, 0.f, nullptr, s);
+  launch_rows_nb<EPI, false, 1, NB, 1, FL>(g, nullptr, nullptr, 0.f, nullptr, s);
 }
 
-// No LayerNorm on A: any instantiated per-split depth.
-template <int EPI>
+// No LayerNorm on A: any instantiated per-split depth; FL_A: A in frag16 (FFN-up's output).
+template <int EPI, int FL = 0>
 void launch_rows(const RowsArgs& g, hipStream_t s) {
   switch (g.K / g.splits / 256) {
-    case 1: launch_rows_plain<EPI, 1>(g, s); return;
-    case 2: launch_rows_plain<EPI, 2>(g, s); return;
-    case 3: launch_rows_plain<EPI, 3>(g, s); return;
-    case 4: launch_rows_plain<EPI, 4>(g, s); return;
-    case 6: launch_rows_plain<EPI, 6>(g, s); return;
-    case 8: launch_rows_plain<EPI, 8>(g, s); return;
-    case 12: launch_rows_plain<EPI, 12>(g, s); return;
-    default: launch_rows_plain<EPI, 16>(g, s); return;
+    case 1: launch_rows_plain<EPI, 1, FL>(g, s); return;
+    case 2: launch_rows_plain<EPI, 2, FL>(g, s); return;
+    case 3: launch_rows_plain<EPI, 3, FL>(g, s); return;
+    case 4: launch_rows_plain<EPI, 4, FL>(g, s); return;
+    case 6: launch_rows_plain<EPI, 6, FL>(g, s); return;
+    case 8: launch_rows_plain<EPI, 8, FL>(g, s); return;
+    case 12: launch_rows_plain<EPI, 12, FL>(g, s); return;
+    default: launch_rows_plain<EPI, 16, FL>(g, s); return;
   }
 }
 
 // A = LN(sum of s_in planes) with K == H, the normalised rows also to ln_out (may be null);
 // s_in = 0: A = LN(embedding sum) gathered by token id (g.ids, g.pos, g.typ).
-template <int EPI, int VPL>
+template <int EPI, int VPL, int FL = 0>
 void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* lnb, float eps,
                     float* ln_out, hipStream_t s) {
   switch (s_in) {
-    case 0: launch_rows_nb<EPI, true, VPL, VPL, 0>(g, lng, lnb, eps, ln_out, s); return;
-    case 1: launch_rows_nb<EPI, true, VPL, VPL, 1>(g, lng, lnb, eps, ln_out, s); return;
-    case 2: launch_rows_nb<EPI, true, VPL, VPL, 2>(g, lng, lnb, eps, ln_out, s); return;
-    case 3: launch_rows_nb<EPI, true, VPL, VPL, 3>(g, lng, lnb, eps, ln_out, s); return;
-    default: launch_rows_nb<EPI, true, VPL, VPL, 4>(g, lng, lnb, eps, ln_out, s); return;
+    case 0: launch_rows_nb<EPI, true, VPL, VPL, 0, FL>(g, lng, lnb, eps, ln_out, s); return;
+    case 1: launch_rows_nb<EPI, true, VPL, VPL, 1, FL>(g, lng, lnb, eps, ln_out, s); return;
+    case 2: launch_rows_nb<EPI, true, VPL, VPL, 2, FL>(g, lng, lnb, eps, ln_out, s); return;
+    case 3: launch_rows_nb<EPI, true, VPL, VPL, 3, FL>(g, lng, lnb, eps, ln_out, s); return;
+    default: launch_rows_nb<EPI, true, VPL, VPL, 4, FL>(g, lng, lnb, eps, ln_out, s); return;
   }
 }
 
-template <int HG>
+template <int HG, bool QF>
 void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
                           int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
                           int ldr, float* out, int64_t o_plane, int nt_w) {
@@ -2158,22 +2262,25 @@ void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, c
                        o_plane, nt_w);
   };
   switch (nkb) {
-    case 1: go(attn_oproj_rows_kernel<HG, 1>); break;
-    case 2: go(attn_oproj_rows_kernel<HG, 2>); break;
-    case 3: go(attn_oproj_rows_kernel<HG, 3>); break;
-    default: go(attn_oproj_rows_kernel<HG, 4>); break;
+    case 1: go(attn_oproj_rows_kernel<HG, 1, QF>); break;
+    case 2: go(attn_oproj_rows_kernel<HG, 2, QF>); break;
+    case 3: go(attn_oproj_rows_kernel<HG, 3, QF>); break;
+    default: go(attn_oproj_rows_kernel<HG, 4, QF>); break;
   }
 }
 
-void launch_attn_oproj(int hg, int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
-                       int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid, int ldr,
-                       float* out, int64_t o_plane, int nt_w) {
-  if (hg == 6)
-    launch_attn_oproj_hg<6>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane,
-                            nt_w);
-  else
-    launch_attn_oproj_hg<4>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane,
-                            nt_w);
+void launch_attn_oproj(int hg, bool qf, int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L,
+                       int H, int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
+                       int ldr, float* out, int64_t o_plane, int nt_w) {
+  auto go = [&](auto hgc, auto qfc) {
+    launch_attn_oproj_hg<decltype(hgc)::value, decltype(qfc)::value>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale,
+                                                                    wo, bo, resid, ldr, out, o_plane, nt_w);
+  };
+  if (hg == 6) {
+    if (qf) go(IC<6>{}, std::true_type{}); else go(IC<6>{}, std::false_type{});
+  } else {
+    if (qf) go(IC<4>{}, std::true_type{}); else go(IC<4>{}, std::false_type{});
+  }
 }
 
 // Heads per output plane of the fused attention + output projection (K3o), 0 = run
@@ -2207,6 +2314,8 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
   const int q_tiles = (L + 31) / 32;
   const int dsplit = rows_splits(F, e->rows_splits);
   const int hg = oproj_heads_per_plane(e, L);
+  // QKV -> K3o through frag16 (Q, K, V^T blocks) when every sequence starts a 16-row block
+  const bool qf = hg != 0 && L % 16 == 0 && (3 * H) % 48 == 0;
   int prev_rows = M;
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
@@ -2215,7 +2324,7 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     const int stride = cls_only ? L * H : H;
     const int nt = (int)li >= e->resident_layers ? 1 : 0;  // this layer's weights bypass MALL
     e->tl.mark(s, ST_QKV);
-    RowsArgs qkv{e->slab.p, H, (int64_t)prev_rows * H, w.wqkv, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1};
+    RowsArgs qkv{e->slab.p, H, (int64_t)prev_rows * H, w.wqkvf, H, w.bqkv, nullptr, 0, e->qkv.p, 3 * H, 0, M, 3 * H, H, 1};
     qkv.nt_w = nt;
     if (li == 0) {  // the embedding gather + LayerNorm run inside the first QKV launch
       qkv.A = e->word;
@@ -2225,11 +2334,15 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       qkv.vocab = c.vocab_size;
       qkv.pos = e->pos;
       qkv.typ = e->typ;
-      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(qkv, 0, e->eg, e->eb, eps, e->x.p, s);
-    } else {
-      const LayerW& p = e->layers[li - 1];
-      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(qkv, dsplit, p.ln2g, p.ln2b, eps, e->x.p, s);
     }
+    const LayerW* pl = li ? &e->layers[li - 1] : nullptr;
+    const float* lg = pl ? pl->ln2g : e->eg;
+    const float* lb = pl ? pl->ln2b : e->eb;
+    const int s_in = pl ? dsplit : 0;
+    if (qf)  // K3o reads Q, K, V^T as whole frag16 blocks
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL, FL_O | FL_OT>(qkv, s_in, lg, lb, eps, e->x.p, s);
+    else
+      ROWS_REP launch_rows_ln<EPI_BIAS, VPL>(qkv, s_in, lg, lb, eps, e->x.p, s);
     const int qt = cls_only ? 1 : q_tiles;
     int y_planes = 1;
     if (hg) {  // attention + output projection in one launch (K3o), hg heads per plane
@@ -2237,7 +2350,7 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       const int rps = cls_only ? 1 : L, qtiles = (rps + 15) / 16;
       y_planes = c.heads / hg;
       const dim3 grid(H / kOpCols, B * qtiles, y_planes);
-      ROWS_REP launch_attn_oproj(hg, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wo, w.bo, e->x.p,
+      ROWS_REP launch_attn_oproj(hg, qf, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wof, w.bo, e->x.p,
                                  stride, e->y.p, (int64_t)rows * H, nt);
     } else {
       e->tl.mark(s, ST_ATTN);
@@ -2247,21 +2360,22 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       else
         launch_attention(B, L, c.heads, qt, H, scale, e->qkv.p, mask, e->ctx.p, s);
       e->tl.mark(s, ST_OPROJ);
-      RowsArgs oproj{e->ctx.p, stride, 0, w.wo, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1};
+      RowsArgs oproj{e->ctx.p, stride, 0, w.wof, H, w.bo, e->x.p, stride, e->y.p, H, 0, rows, H, H, 1};
       oproj.nt_w = nt;
       launch_rows<EPI_RESID>(oproj, s);
     }
     e->tl.mark(s, ST_FFN_UP);
-    RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
+    // FFN-up writes the GELU rows in frag16 for FFN-down's A operand
+    RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1f, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
     up.nt_w = nt;
     if (c.gelu == MQ_GELU_TANH)
-      ROWS_REP launch_rows_ln<EPI_GELU_TANH, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_GELU_TANH, VPL, FL_O>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     else
-      ROWS_REP launch_rows_ln<EPI_GELU_ERF, VPL>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
+      ROWS_REP launch_rows_ln<EPI_GELU_ERF, VPL, FL_O>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     e->tl.mark(s, ST_FFN_DOWN);
-    RowsArgs down{e->ffn.p, F, 0, w.w2, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F, dsplit};
+    RowsArgs down{e->ffn.p, F, 0, w.w2f, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F, dsplit};
     down.nt_w = nt;
-    ROWS_REP launch_rows<EPI_RESID>(down, s);
+    ROWS_REP launch_rows<EPI_RESID, FL_A>(down, s);
     prev_rows = rows;
   }
   e->tl.mark(s, ST_POOL);
@@ -2281,7 +2395,8 @@ bool use_rows_path(const mq_encoder* e, int B, int L) {
   const int sp = rows_splits(c.ffn, e->rows_splits);
   // slab holds the FFN-down planes: splits x rows x H floats
   return (int64_t)B * L <= e->rows_max && !e->layers.empty() && c.ffn % 256 == 0 &&
-         rows_nb_ok(c.ffn / 256 / sp) && (size_t)sp * B * L * c.hidden <= e->slab.n;
+         rows_nb_ok(c.ffn / 256 / sp) && (size_t)sp * B * L * c.hidden <= e->slab.n &&
+         e->layers[0].wqkvf != nullptr;  // (the frag16 weight images)
 }
 
 }  // namespace
@@ -2306,7 +2421,7 @@ constexpr size_t kMaxGraphs = 6;
 int launch_graph(mq_encoder* e, int B, int L, hipStream_t s) {
   const std::vector<const void*> bufs = {e->weights.p, e->x.p,   e->y.p,      e->qkv.p,
                                          e->ctx.p,     e->ffn.p, e->slab.p,   e->io_out.p,
-                                         e->io_ids,    e->io_mask,  e->w3.p};
+                                         e->io_ids,    e->io_mask,  e->w3.p,   e->wfrag.p};
   mq_encoder::Graph* hit = nullptr;
   for (auto& g : e->graphs)
     if (g.B == B && g.L == L && g.precision == e->precision && g.bufs == bufs) hit = &g;
@@ -2393,7 +2508,8 @@ int mq_encoder_destroy(mq_encoder* e) {
   if (!e) return MQ_OK;
   {
     DeviceGuard dg(e->device);
-    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab})
+    for (Buf* b : {&e->weights, &e->x, &e->y, &e->qkv, &e->ctx, &e->ffn, &e->io_out, &e->slab, &e->w3, &e->wfrag,
+                   &e->lnst})
       b->release();
     if (e->io_ids) (void)hipFree(e->io_ids);
     if (e->io_mask) (void)hipFree(e->io_mask);
@@ -2447,6 +2563,10 @@ int mq_encoder_load_weights(mq_encoder* e, const float* blob, int64_t n_floats) 
     e->layers.push_back(w);
   }
   e->loaded = true;
+  if (H % 16 == 0 && F % 16 == 0) {  // (the few-row path needs them: use_rows_path checks)
+    rc = build_frag16(e);
+    if (rc) return rc;
+  }
   return build_w3(e);  // (re)split the new weights when the split-f32 precision is selected
 }
 
@@ -2627,7 +2747,8 @@ int mq_encoder_embed(mq_encoder* e, const int32_t* ids, const int32_t* mask, int
   const size_t ln_parts = e->ln_on_load && M > 256 ? (size_t)4 * M * std::max(1, c.hidden / kLnPartW) : 0;
   for (auto bn : {std::make_pair(&e->x, M * c.hidden), std::make_pair(&e->y, (M <= (size_t)kRowsMax ? 4 : 1) * M * c.hidden),
                   std::make_pair(&e->ctx, M * c.hidden), std::make_pair(&e->qkv, M * 3 * c.hidden),
-                  std::make_pair(&e->ffn, M * c.ffn), std::make_pair(&e->lnst, ln_parts)}) {
+                  // (the few-row FFN output is frag16: whole 16-row blocks)
+                  std::make_pair(&e->ffn, (M + 15) / 16 * 16 * c.ffn), std::make_pair(&e->lnst, ln_parts)}) {
     rc = bn.first->ensure(bn.second);
     if (rc) return rc;
   }

@@ -572,7 +572,10 @@ __global__ __launch_bounds__(256) void screen_verify_kernel(const float* __restr
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   const float E = screen_bound(Q, dim, q, mode, stats, lane);
-  const bool failed = !(cs[q * kc + kc - 1] + E < es[q * k + k - 1]);  // wave-uniform
+  // cs_kc = -inf: the scan kept fewer than kc rows with tau = -inf, i.e. every row it
+  // could see (a filter's allowed rows) is a candidate - the re-rank is the exact answer
+  const float ckc = cs[q * kc + kc - 1];
+  const bool failed = !(ckc + E < es[q * k + k - 1]) && ckc != -INFINITY;  // wave-uniform
   if (!failed) return;
   int slot = 0;
   if (lane == 0) {
@@ -641,17 +644,20 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ Q
       sid[c0 + slot] = my_id;
     }
   }
+  // every slot starts as padding: the padding candidates (id -1, fewer real candidates than
+  // k - a filter admitting few rows, or k > kc) all rank alike and write no slot below
+  if (tid < k) {
+    out_s[q * k + tid] = -INFINITY;
+    out_i[q * k + tid] = -1;
+  }
   __syncthreads();
-  if (tid < kc) {
+  if (tid < kc && sid[tid] >= 0) {
     int rank = 0;
     for (int u = 0; u < kc; ++u) rank += better(sc[u], sid[u], sc[tid], sid[tid]) ? 1 : 0;
     if (rank < k) {
-      out_s[q * k + rank] = sid[tid] >= 0 ? sc[tid] : -INFINITY;
+      out_s[q * k + rank] = sc[tid];
       out_i[q * k + rank] = sid[tid];
     }
-  } else if (tid < k) {
-    out_s[q * k + tid] = -INFINITY;  // k > kc: padding past the candidates
-    out_i[q * k + tid] = -1;
   }
 }
 
