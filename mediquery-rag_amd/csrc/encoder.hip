@@ -1172,6 +1172,8 @@ __global__ __launch_bounds__(64 * NS * HB, NS == 1 && HB == 1 ? 3 : 1) void atte
     m_run = m_new;
     o0 *= alpha;
     o1 *= alpha;
+    // (V staged through this LDS tile by whole-line loads instead, in flight under the
+    // softmax, measured slower: attention 0.298 -> 0.327 ms per step, r6)
     const float* vbase = qkv + row0 * ld + 2 * H + h * kDh + r;
 #pragma unroll
     for (int sidx = 0; sidx < 16; ++sidx) {
