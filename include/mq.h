@@ -341,7 +341,9 @@ int64_t mq_debug_w3_bytes(int N, int K);
 int mq_debug_split_w3(const float* W, int N, int K, void* w3, void* stream);
 /* The encoder GEMM on the pre-split split-f32 kernel (K2p) with W given as its W3 image:
  * tile 0 = 128x192, 1 = 256x96 (4 compute + 4 loader waves), 2 = 128x192, 3 = 256x192
- * (8 compute waves), -1 = the default pick; 4-7 = measurement variants (gemm_x6p.hip).
+ * (8 compute waves), -1 = the default pick; 4-7 = measurement variants (gemm_x6p.hip);
+ * codes >= 100: tile code % 100 with the tile walk cut into one region per XCD,
+ * code / 100 - 1 column blocks (0 = the plain round-robin walk; below 100: the pick).
  * Bit-identical to the split-f32 tiles 5-7 / 9 of mq_debug_gemm_f32.  Asynchronous on
  * `stream`.  K % 32 == 0. */
 int mq_debug_gemm_x6p(const float* A, const void* W3, const float* bias, const float* resid,

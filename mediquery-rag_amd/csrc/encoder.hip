@@ -175,22 +175,30 @@ __global__ __launch_bounds__(T::THREADS, T::WG_PER_CU) void gemm_nt_kernel(const
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ resid, int ldr,
                                                          float* __restrict__ out, int ldo, int M,
-                                                         int N, int K, LnArgs ln) {
+                                                         int N, int K, LnArgs ln, int rx) {
   __shared__ __attribute__((aligned(16))) float lds[2 * T::STAGE_FLOATS];
   __shared__ float2 ln_st[LN_IN ? 2 * T::BM : 1];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
-  const int tiles_n = (N + T::BN - 1) / T::BN;
-  const int total = ((M + T::BM - 1) / T::BM) * tiles_n;
+  const int tiles_n = (N + T::BN - 1) / T::BN, tiles_m = (M + T::BM - 1) / T::BM;
   const int G = gridDim.x, per_xcd = G >> 3;
   const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
-  const FastDiv tnd(tiles_n);
+  // rx > 0: region walk (gemm_x6p.hpp region_of): this XCD group's tiles, row-major in it
+  Region rg{0, tiles_m, 0, tiles_n};
+  int loc = xslot, wstep = G;
+  if (rx > 0) {
+    rg = region_of(rx, blockIdx.x & 7, tiles_m, tiles_n);
+    loc = blockIdx.x >> 3;
+    wstep = per_xcd;
+  }
+  const int rtiles = rg.rm * rg.rn;
+  const int n_tiles = loc < rtiles ? (rtiles - loc + wstep - 1) / wstep : 0;
+  const FastDiv tnd(rg.rn);
   auto coords = [&](int i, int& m0, int64_t& n0) {
-    const int t = i * G + xslot;
+    const int t = i * wstep + loc;
     const int tr = tnd.div(t);
-    m0 = tr * T::BM;
-    n0 = (int64_t)(t - tr * tiles_n) * T::BN;
+    m0 = (rg.m_lo + tr) * T::BM;
+    n0 = (int64_t)(rg.n_lo + t - tr * rg.rn) * T::BN;
   };
   auto epi = [&](int i, floatx16(&acc)[T::TM][T::TN], float*) {
     int m0;
@@ -1713,8 +1721,10 @@ void launch_gemm_t(const GemmArgs& g, int num_cus, hipStream_t s, const LnArgs& 
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
   // persistent grid: the workgroups that fit the CUs at once, a multiple of 8
   const int grid = (std::min(tiles, T::WG_PER_CU * num_cus) + 7) / 8 * 8;
+  const int tiles_m = (g.M + T::BM - 1) / T::BM, tiles_n = (g.N + T::BN - 1) / T::BN;
+  const int rx = region_pick_rx(tiles_m, tiles_n, (double)T::BM * g.K * 4, (double)T::BN * g.K * 4, grid);
   hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, LN_IN>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda, g.W,
-                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K, ln);
+                     g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K, ln, rx);
 }
 
 using GemmBig = F32Tile<2, 2, 2, 2>;    // 128 x 128

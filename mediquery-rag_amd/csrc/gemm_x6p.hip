@@ -134,7 +134,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void gemm_x6p_kernel(const float* __
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ resid, int ldr,
                                                              float* __restrict__ out, int ldo, int M, int N,
-                                                             int K) {
+                                                             int K, int rx) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[T::NBUF * T::STAGE];
   const unsigned lds0 = (unsigned)(uintptr_t)(x6p_lds_t*)lds;
   const int lane = threadIdx.x & 63;
@@ -145,21 +145,36 @@ __global__ __launch_bounds__(T::THREADS, 1) void gemm_x6p_kernel(const float* __
   const int total = tiles_m * tiles_n;
   const int G = gridDim.x, per_xcd = G >> 3;
   const int xslot = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int n_tiles = xslot < total ? (total - xslot + G - 1) / G : 0;
+  // rx > 0: the tile grid is cut into 8 regions, rx column blocks x 8 / rx row blocks, and
+  // the workgroups that share blockIdx.x % 8 (an XCD under round-robin dispatch; a speed
+  // assumption, never a correctness one) walk one region - its W3 column panels stay in
+  // that XCD's L2 for the whole launch instead of being re-read every round
+  int m_lo = 0, rm = tiles_m, n_lo = 0, rn = tiles_n, loc = xslot, wstep = G, rtiles = total;
+  if (rx > 0) {
+    const Region rg = region_of(rx, blockIdx.x & 7, tiles_m, tiles_n);
+    m_lo = rg.m_lo;
+    rm = rg.rm;
+    n_lo = rg.n_lo;
+    rn = rg.rn;
+    loc = blockIdx.x >> 3;
+    wstep = per_xcd;
+    rtiles = rm * rn;
+  }
+  const int n_tiles = loc < rtiles ? (rtiles - loc + wstep - 1) / wstep : 0;
   if (n_tiles == 0) return;
   const int nk = K >> 4;                 // 16-deep k-steps per tile
   const int nst = nk / T::KS;            // stages per tile (the launcher checks K % (16 KS) == 0)
   const int S = n_tiles * nst;           // stages of this workgroup
   const int nbw = (N + 31) >> 5;
-  const int band_tiles = T::GM * tiles_n;
-  auto coords = [&](int i, int& m0, int& n0) {
-    const int t = i * G + xslot;
+  const int band_tiles = T::GM * rn;
+  auto coords = [&](int i, int& m0, int& n0) {  // bands of GM row tiles, column-major inside
+    const int t = i * wstep + loc;
     const int band = t / band_tiles;
-    const int gm = min(T::GM, tiles_m - band * T::GM);
+    const int gm = min(T::GM, rm - band * T::GM);
     const int w = t - band * band_tiles;
     const int tc = w / gm;
-    m0 = (band * T::GM + (w - tc * gm)) * T::BM;
-    n0 = tc * T::BN;
+    m0 = (m_lo + band * T::GM + (w - tc * gm)) * T::BM;
+    n0 = (n_lo + tc) * T::BN;
   };
 
   // ---- DMA issue of stage `is_j` into a ring slot (past the last stage: the last again,
@@ -521,8 +536,12 @@ void launch_t(const X6pArgs& g, int num_cus, hipStream_t s) {
   }
   const int tiles = ((g.M + T::BM - 1) / T::BM) * ((g.N + T::BN - 1) / T::BN);
   const int grid = (std::min(tiles, num_cus) + 7) / 8 * 8;  // one workgroup per CU, a multiple of 8
+  const int tiles_m = (g.M + T::BM - 1) / T::BM, tiles_n = (g.N + T::BN - 1) / T::BN;
+  int rx = g.rx;
+  if (rx < 0) rx = region_pick_rx(tiles_m, tiles_n, (double)T::BM * g.K * 4, (double)T::BN * g.K * 6, grid);
+  if (rx > 0 && (8 % rx != 0 || rx > tiles_n || 8 / rx > tiles_m || grid < 8)) rx = 0;  // (a region per XCD)
   hipLaunchKernelGGL((gemm_x6p_kernel<T, EPI>), dim3(grid), dim3(T::THREADS), 0, s, g.A, g.lda,
-                     static_cast<const unsigned char*>(g.W3), g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K);
+                     static_cast<const unsigned char*>(g.W3), g.bias, g.resid, g.ldr, g.out, g.ldo, g.M, g.N, g.K, rx);
 }
 
 template <int EPI>
@@ -613,11 +632,17 @@ int mq_debug_gemm_x6p(const float* A, const void* W3, const float* bias, const f
   clear_error();
   MQ_CHECK_ARG(A && W3 && bias && out && (epi != EPI_RESID || resid), "NULL buffer");
   MQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 32 == 0, "bad shape M=%d N=%d K=%d", M, N, K);
-  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= -1 && tile <= 15, "bad epi/tile");
+  // tile codes >= 100: tile code % 100 with the region split rx = code / 100 - 1 (0 = the
+  // plain walk); below 100 the automatic pick
+  const int rx = tile >= 100 ? tile / 100 - 1 : -1;
+  if (tile >= 100) tile %= 100;
+  MQ_CHECK_ARG(epi >= 0 && epi <= 3 && tile >= -1 && tile <= 15 && rx <= 8, "bad epi/tile");
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  launch_gemm_x6p(X6pArgs{A, K, W3, bias, resid, N, out, N, M, N, K}, epi, tile, cus, (hipStream_t)stream);
+  X6pArgs g{A, K, W3, bias, resid, N, out, N, M, N, K};
+  g.rx = rx;
+  launch_gemm_x6p(g, epi, tile, cus, (hipStream_t)stream);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }

@@ -28,6 +28,45 @@ inline size_t w3_bytes(int64_t N, int64_t K) { return (size_t)((N + 31) / 32) * 
 // image of rows [row0, N) of W is the tail of W's image
 inline size_t w3_row_offset(int64_t row0, int64_t K) { return (size_t)(row0 / 32) * (size_t)(K / 16) * 3 * 1024; }
 
+// Region split of a persistent GEMM's tile walk: the tile grid cut into 8 regions, rx
+// column blocks x 8 / rx row blocks, one walked by the workgroups sharing blockIdx.x % 8
+// (one XCD under round-robin dispatch: speed only), so an XCD's weight column panels stay
+// in its L2 across rounds instead of every round re-reading them.  The pick: the rx with
+// the fewest per-XCD operand bytes (its A row panels + its W column panels), 0 (the plain
+// round-robin walk) when every workgroup has at most one tile.  r6, K2p at M = 8192: QKV
+// 152.8 -> 134.9 us (rx 4) / 138.4 (rx 2, the pick), the other shapes unchanged
+// (profiles/r6/ab_x6p_regions/).
+inline int region_pick_rx(int64_t tiles_m, int64_t tiles_n, double a_bytes_per_row_tile,
+                          double w_bytes_per_col_tile, int64_t grid) {
+  if (tiles_m * tiles_n <= grid || grid < 8) return 0;
+  int best = 0;
+  double best_b = 0;
+  for (int rx = 1; rx <= 8; rx *= 2) {
+    const int ry = 8 / rx;
+    if (rx > tiles_n || ry > tiles_m) continue;
+    const double b = (double)((tiles_m + ry - 1) / ry) * a_bytes_per_row_tile +
+                     (double)((tiles_n + rx - 1) / rx) * w_bytes_per_col_tile;
+    if (best == 0 || b < best_b) {
+      best = rx;
+      best_b = b;
+    }
+  }
+  return best;
+}
+// the region [m_lo, m_lo + rm) x [n_lo, n_lo + rn) of tiles walked by XCD group xc (rx > 0)
+struct Region {
+  int m_lo, rm, n_lo, rn;
+};
+__host__ __device__ inline Region region_of(int rx, int xc, int tiles_m, int tiles_n) {
+  const int ry = 8 / rx, ri = xc / rx, rj = xc - ri * rx;
+  Region r;
+  r.m_lo = ri * tiles_m / ry;
+  r.rm = (ri + 1) * tiles_m / ry - r.m_lo;
+  r.n_lo = rj * tiles_n / rx;
+  r.rn = (rj + 1) * tiles_n / rx - r.n_lo;
+  return r;
+}
+
 // split W [N][K] fp32 (row stride K) into its W3 image (w3_bytes(N, K) bytes)
 void launch_split_w3(const float* W, int N, int K, void* w3, hipStream_t s);
 
@@ -41,6 +80,7 @@ struct X6pArgs {
   float* out;
   int ldo;
   int M, N, K;  // K % 16 == 0
+  int rx = -1;  // tile-walk region split (gemm_x6p.hip x6p_pick_rx): -1 = the pick, 0 = none, 1/2/4/8
 };
 
 // Tile shapes (workgroups of 8 waves, one per CU): 0 = 128 x 192 (4 compute + 4 loader
