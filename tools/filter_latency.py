@@ -4,7 +4,10 @@ metadata carries a 16-value `tag` and an integer `n`; the filter passes ~1/2 or 
 the rows.  Reports p50 ms for: no filter, a repeated filter and a fresh filter every call
 (r5: the where-mask built on the device from the metadata code columns, then the masked
 int8 certified search; r3/r4 gathered the allowed rows through a host row list), and the
-masked searches that fell back to the device gather.
+masked searches that fell back to the device gather.  r6: the 256-query batched filtered
+search (`similarity_search_batch(filter=)`: ONE masked call - the bf16 threshold scan with
+the row mask) against the unfiltered 256-query batch, and `delete` of 1k ids with the store
+in memory (auto_persist off: the device compaction + the host lists, no slab rewrite).
 
   python tools/filter_latency.py [--rows 1000000] [--iters 50]
 """
@@ -60,9 +63,18 @@ def main():
     out["fresh_filter_half_ms"] = p50(
         lambda i: store.similarity_search_by_vector(qs[i % 64], k=5, filter={"n": {"$lt": 40 + i % 20}}), args.iters)
     out["masked_gathers"] = store._index.masked_gathers
+    # batches of 256 query vectors: one device search / one masked call for all of them
+    qb = emb[rng.integers(0, n, 256)] + 0.01 * rng.standard_normal((256, 768)).astype(np.float32)
+    ix = store._index
+    out["batch256_unfiltered_ms"] = p50(lambda i: ix.search(qb, 5), 10)
+    for name, f in (("half", {"n": {"$lt": 50}}), ("16th", {"tag": "t3"})):
+        g0 = ix.masked_gathers
+        out["batch256_filter_%s_ms" % name] = p50(lambda i, f=f: ix.search_masked(qb, 5, store._cols.dmask(f, 0)), 10)
+        out["batch256_filter_%s_uncertified" % name] = ix.masked_gathers - g0
+        out["batch256_filter_%s_ratio" % name] = round(out["batch256_filter_%s_ms" % name] / out["batch256_unfiltered_ms"], 2)
     t0 = time.perf_counter()
     store.delete(["id%d" % i for i in range(0, n, 1000)])
-    out["delete_1k_of_n_s"] = round(time.perf_counter() - t0, 3)
+    out["delete_1k_of_n_s"] = round(time.perf_counter() - t0, 4)
     print(json.dumps(out), flush=True)
 
 
