@@ -285,6 +285,10 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
  *                                weights' W3 plane images (split once, at weight load or
  *                                set_precision), 0 = the split-f32 tiles that split both
  *                                operands while staging them.  Bit-identical results.
+ *   MQ_ENC_OPT_ROWS_PLANES       few-row forward: 0 (default) = FFN-down's two K splits and the
+ *                                fused attention's two head groups add into ONE output plane
+ *                                (two addends per element: bitwise the sum the consumer took), so
+ *                                the next QKV / FFN-up reads one plane of rows; 1 = two planes.
  * Setting an option drops the handle's captured graphs. */
 #define MQ_ENC_OPT_ROWS_MAX 0
 #define MQ_ENC_OPT_ROWS_SPLITS 1
@@ -296,6 +300,7 @@ int mq_encoder_set_graphs(mq_encoder* enc, int enabled);
 #define MQ_ENC_OPT_LN_ON_LOAD 7
 #define MQ_ENC_OPT_RESIDENT_LAYERS 8
 #define MQ_ENC_OPT_X6_PRESPLIT 9
+#define MQ_ENC_OPT_ROWS_PLANES 10
 int mq_encoder_set_option(mq_encoder* enc, int option, int value);
 int mq_encoder_get_option(const mq_encoder* enc, int option, int* value);
 int mq_encoder_set_timing(mq_encoder* enc, int enabled);

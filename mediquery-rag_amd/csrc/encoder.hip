@@ -770,7 +770,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const float* W) {
 // in this layout for FFN-down (FL_O / FL_A).
 // FL_OT (with FL_O): the blocks of the last third of the columns (QKV's V) are stored
 // transposed - the frag16 of V^T - so attention's P V reads V^T fragments whole
-enum RowsFlags { FL_A = 1, FL_O = 2, FL_OT = 4 };  // A in frag16 / output in frag16 (weights always are)
+// FL_ACC: the K splits add into ONE output plane (a no-return device-scope atomic add per
+// element into a zeroed buffer) instead of writing a plane each.  With exactly two addends
+// per element, 0 + a + b and 0 + b + a are the same float (addition commutes), so the result
+// is bitwise the p0 + p1 the consumer summed before - and the consumer reads one plane.
+enum RowsFlags { FL_A = 1, FL_O = 2, FL_OT = 4, FL_ACC = 8 };  // A / output in frag16 (weights always are)
 __device__ __forceinline__ int64_t frag16_offset(int64_t row, int col, int cols) {  // in floats
   return ((row >> 4) * (cols >> 4) + (col >> 4)) * 256 + ((row & 15) + 16 * ((col & 15) >> 2)) * 4 + (col & 3);
 }
@@ -800,8 +804,16 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
     const float* __restrict__ W, int ldw, const float* __restrict__ bias,
     const float* __restrict__ resid, int ldr, float* __restrict__ out, int ldo, int64_t o_plane,
     const int* __restrict__ ids, int L, int vocab, const float* __restrict__ pos,
-    const float* __restrict__ typ, int nt_w) {
+    const float* __restrict__ typ, int nt_w, float* __restrict__ zbuf, int64_t zn) {
   static_assert(!(LN_IN && (FL & FL_A)), "a LayerNorm input is read row-major");
+  static_assert(!((FL & FL_ACC) && (FL & FL_O)), "accumulated output is row-major");
+  // zbuf: zn floats (a multiple of 4) this launch zeroes for a LATER launch's FL_ACC adds
+  if (zbuf) {
+    const int64_t nwg = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+    const int64_t wg = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    for (int64_t i = wg * 1024 + threadIdx.x; i < zn / 4; i += nwg * 1024)
+      reinterpret_cast<floatx4*>(zbuf)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
   constexpr int K = NB * 256;  // depth of this workgroup's K split (blockIdx.z)
   // 16-deep blocks per load batch: all of them while the operands fit the 128 VGPRs of a
   // 1024-thread workgroup (one memory round trip), else batches
@@ -985,6 +997,8 @@ __global__ __launch_bounds__(1024) void rows_gemm_kernel(
   }
   if (FL & FL_O)
     out[ks * o_plane + (((int64_t)((r0 >> 4) + ert) * (ldo >> 4) + blockIdx.x) << 8) + ep] = v;
+  else if (FL & FL_ACC)
+    (void)atomicAdd(out + (int64_t)erow * ldo + ecol, v);
   else
     out[ks * o_plane + (int64_t)erow * ldo + ecol] = v;
   KTRACE_R(EPI == EPI_BIAS ? 0 : EPI == EPI_RESID ? 2 : 1, 5);
@@ -1376,7 +1390,8 @@ constexpr int kOpCols = 32;  // output columns per workgroup
 
 // QF: qkv in frag16 with V^T blocks (QKV's FL_O | FL_OT; needs L % 16 == 0, so every
 // sequence starts a 16-row block): Q, K and V^T fragments load as whole 1 KB blocks.
-template <int HG, int NKB, bool QF = false>
+// ACC: the head groups add into ONE zeroed output plane (two groups: FL_ACC's argument).
+template <int HG, int NKB, bool QF = false, bool ACC = false>
 __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
     const float* __restrict__ qkv, const int* __restrict__ mask, int L, int H, int rps, int qtiles,
     float scale, const float* __restrict__ Wo, const float* __restrict__ bo,
@@ -1552,7 +1567,10 @@ __global__ __launch_bounds__(512) void attn_oproj_rows_kernel(
   for (int q = 1; q < 4; ++q) v += part[ecb + 2 * q][e];
   if (qrow >= rps) return;
   if (grp == 0) v = (v + ebias) + eres;
-  out[grp * o_plane + orow * H + ecol] = v;
+  if (ACC)
+    (void)atomicAdd(out + orow * H + ecol, v);
+  else
+    out[grp * o_plane + orow * H + ecol] = v;
   KTRACE_R(3, 6);
 }
 
@@ -1922,6 +1940,7 @@ struct mq_encoder {
                                 // measured slower: the consumers' staging VALU)
   Buf lnst;                     // its per-row partials, two sets of [M][H / kLnPartW] (mean, M2)
   bool x6_presplit = true;      // split-f32 batched GEMMs on the W3 images (K2p)
+  bool rows_planes = false;     // few-row forward: keep the two-plane hand-offs (no FL_ACC merge)
   bool use_graphs = false;  // eager measured faster for one query (0.628 vs 0.645 ms: the
                             // graph path stages ids / mask / out through its own buffers)
   uint64_t graph_clock = 0;
@@ -2187,6 +2206,8 @@ struct RowsArgs {
   const float* pos = nullptr;
   const float* typ = nullptr;
   int nt_w = 0;  // weights loaded non-temporally (layers past resident_layers)
+  float* zbuf = nullptr;  // zn floats this launch zeroes for a later launch's FL_ACC adds
+  int64_t zn = 0;
 };
 
 // Row tiles per workgroup: two for the LayerNorm-input GEMMs when M > 16 (the launch then
@@ -2200,7 +2221,7 @@ void launch_rows_rt(const RowsArgs& g, const float* lng, const float* lnb, float
   hipLaunchKernelGGL((rows_gemm_kernel<EPI, LN_IN, VPL, NB, S_IN, RT, FL>),
                      dim3(g.N / kRT, (g.M + kRT * RT - 1) / (kRT * RT), g.splits), dim3(64 * kRWaves), 0, s,
                      g.A, g.lda, g.a_plane, g.M, lng, lnb, eps, ln_out, g.W, g.ldw, g.bias, g.resid, g.ldr,
-                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ, g.nt_w);
+                     g.out, g.ldo, g.o_plane, g.ids, g.L, g.vocab, g.pos, g.typ, g.nt_w, g.zbuf, g.zn);
 }
 
 template <int EPI, bool LN_IN, int VPL, int NB, int S_IN, int FL = 0>
@@ -2265,7 +2286,7 @@ void launch_rows_ln(const RowsArgs& g, int s_in, const float* lng, const float* 
   }
 }
 
-template <int HG, bool QF>
+template <int HG, bool QF, bool ACC>
 void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L, int H,
                           int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
                           int ldr, float* out, int64_t o_plane, int nt_w) {
@@ -2274,24 +2295,29 @@ void launch_attn_oproj_hg(int nkb, dim3 grid, hipStream_t s, const float* qkv, c
                        o_plane, nt_w);
   };
   switch (nkb) {
-    case 1: go(attn_oproj_rows_kernel<HG, 1, QF>); break;
-    case 2: go(attn_oproj_rows_kernel<HG, 2, QF>); break;
-    case 3: go(attn_oproj_rows_kernel<HG, 3, QF>); break;
-    default: go(attn_oproj_rows_kernel<HG, 4, QF>); break;
+    case 1: go(attn_oproj_rows_kernel<HG, 1, QF, ACC>); break;
+    case 2: go(attn_oproj_rows_kernel<HG, 2, QF, ACC>); break;
+    case 3: go(attn_oproj_rows_kernel<HG, 3, QF, ACC>); break;
+    default: go(attn_oproj_rows_kernel<HG, 4, QF, ACC>); break;
   }
 }
 
-void launch_attn_oproj(int hg, bool qf, int nkb, dim3 grid, hipStream_t s, const float* qkv, const int* mask, int L,
-                       int H, int rps, int qtiles, float scale, const float* wo, const float* bo, const float* resid,
-                       int ldr, float* out, int64_t o_plane, int nt_w) {
-  auto go = [&](auto hgc, auto qfc) {
-    launch_attn_oproj_hg<decltype(hgc)::value, decltype(qfc)::value>(nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale,
-                                                                    wo, bo, resid, ldr, out, o_plane, nt_w);
+// acc: the two head-group planes added into one zeroed plane (hg = heads / 2 only)
+void launch_attn_oproj(int hg, bool qf, bool acc, int nkb, dim3 grid, hipStream_t s, const float* qkv,
+                       const int* mask, int L, int H, int rps, int qtiles, float scale, const float* wo,
+                       const float* bo, const float* resid, int ldr, float* out, int64_t o_plane, int nt_w) {
+  auto go = [&](auto hgc, auto qfc, auto accc) {
+    launch_attn_oproj_hg<decltype(hgc)::value, decltype(qfc)::value, decltype(accc)::value>(
+        nkb, grid, s, qkv, mask, L, H, rps, qtiles, scale, wo, bo, resid, ldr, out, o_plane, nt_w);
   };
   if (hg == 6) {
-    if (qf) go(IC<6>{}, std::true_type{}); else go(IC<6>{}, std::false_type{});
+    if (qf && acc) go(IC<6>{}, std::true_type{}, std::true_type{});
+    else if (qf) go(IC<6>{}, std::true_type{}, std::false_type{});
+    else if (acc) go(IC<6>{}, std::false_type{}, std::true_type{});
+    else go(IC<6>{}, std::false_type{}, std::false_type{});
   } else {
-    if (qf) go(IC<4>{}, std::true_type{}); else go(IC<4>{}, std::false_type{});
+    if (qf) go(IC<4>{}, std::true_type{}, std::false_type{});
+    else go(IC<4>{}, std::false_type{}, std::false_type{});
   }
 }
 
@@ -2328,6 +2354,11 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
   const int hg = oproj_heads_per_plane(e, L);
   // QKV -> K3o through frag16 (Q, K, V^T blocks) when every sequence starts a 16-row block
   const bool qf = hg != 0 && L % 16 == 0 && (3 * H) % 48 == 0;
+  // two-addend plane merges (FL_ACC): FFN-down's two K splits and K3o's two head groups add
+  // into one zeroed plane, so QKV and FFN-up read one plane of rows instead of two (the
+  // buffer each zeroes: the slab by FFN-up, y by QKV, a launch ahead of the adds)
+  const bool dacc = dsplit == 2 && !e->rows_planes;
+  const bool yacc = hg != 0 && c.heads / hg == 2 && !e->rows_planes;
   int prev_rows = M;
   for (size_t li = 0; li < e->layers.size(); ++li) {
     const LayerW& w = e->layers[li];
@@ -2350,7 +2381,11 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     const LayerW* pl = li ? &e->layers[li - 1] : nullptr;
     const float* lg = pl ? pl->ln2g : e->eg;
     const float* lb = pl ? pl->ln2b : e->eb;
-    const int s_in = pl ? dsplit : 0;
+    const int s_in = pl ? (dacc ? 1 : dsplit) : 0;
+    if (yacc) {  // K3o of this layer adds into y
+      qkv.zbuf = e->y.p;
+      qkv.zn = (int64_t)rows * H;
+    }
     if (qf)  // K3o reads Q, K, V^T as whole frag16 blocks
       ROWS_REP launch_rows_ln<EPI_BIAS, VPL, FL_O | FL_OT>(qkv, s_in, lg, lb, eps, e->x.p, s);
     else
@@ -2362,7 +2397,8 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
       const int rps = cls_only ? 1 : L, qtiles = (rps + 15) / 16;
       y_planes = c.heads / hg;
       const dim3 grid(H / kOpCols, B * qtiles, y_planes);
-      ROWS_REP launch_attn_oproj(hg, qf, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wof, w.bo, e->x.p,
+      if (yacc) y_planes = 1;
+      ROWS_REP launch_attn_oproj(hg, qf, yacc, (L + 15) / 16, grid, s, e->qkv.p, mask, L, H, rps, qtiles, scale, w.wof, w.bo, e->x.p,
                                  stride, e->y.p, (int64_t)rows * H, nt);
     } else {
       e->tl.mark(s, ST_ATTN);
@@ -2380,6 +2416,10 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     // FFN-up writes the GELU rows in frag16 for FFN-down's A operand
     RowsArgs up{e->y.p, H, (int64_t)rows * H, w.w1f, H, w.b1, nullptr, 0, e->ffn.p, F, 0, rows, F, H, 1};
     up.nt_w = nt;
+    if (dacc) {  // FFN-down of this layer adds into the slab
+      up.zbuf = e->slab.p;
+      up.zn = (int64_t)rows * H;
+    }
     if (c.gelu == MQ_GELU_TANH)
       ROWS_REP launch_rows_ln<EPI_GELU_TANH, VPL, FL_O>(up, y_planes, w.ln1g, w.ln1b, eps, e->x.p, s);
     else
@@ -2387,13 +2427,16 @@ int forward_rows(mq_encoder* e, const int* ids, const int* mask, int B, int L, f
     e->tl.mark(s, ST_FFN_DOWN);
     RowsArgs down{e->ffn.p, F, 0, w.w2f, F, w.b2, e->x.p, H, e->slab.p, H, (int64_t)rows * H, rows, H, F, dsplit};
     down.nt_w = nt;
-    ROWS_REP launch_rows<EPI_RESID, FL_A>(down, s);
+    if (dacc)
+      ROWS_REP launch_rows<EPI_RESID, FL_A | FL_ACC>(down, s);
+    else
+      ROWS_REP launch_rows<EPI_RESID, FL_A>(down, s);
     prev_rows = rows;
   }
   e->tl.mark(s, ST_POOL);
   const LayerW& last = e->layers.back();
   const int pool_rows = c.pooling == MQ_POOL_CLS ? 1 : L;  // slab holds [B, H] CLS rows or [M, H]
-  hipLaunchKernelGGL((ln_pool_kernel<VPL>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, e->slab.p, dsplit,
+  hipLaunchKernelGGL((ln_pool_kernel<VPL>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, e->slab.p, dacc ? 1 : dsplit,
                      (int64_t)prev_rows * H, mask, B, L, pool_rows, c.pooling, last.ln2g, last.ln2b, eps, out);
   e->tl.close(s);
   MQ_HIP(hipGetLastError());
@@ -2688,6 +2731,10 @@ int mq_encoder_set_option(mq_encoder* e, int option, int value) {
       MQ_CHECK_ARG(value == 0 || value == 1, "x6_presplit must be 0 or 1 (got %d)", value);
       e->x6_presplit = value != 0;
       break;
+    case MQ_ENC_OPT_ROWS_PLANES:
+      MQ_CHECK_ARG(value == 0 || value == 1, "rows_planes must be 0 or 1 (got %d)", value);
+      e->rows_planes = value != 0;
+      break;
     default:
       MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
@@ -2711,6 +2758,7 @@ int mq_encoder_get_option(const mq_encoder* e, int option, int* value) {
     case MQ_ENC_OPT_RESIDENT_LAYERS: *value = e->resident_layers; break;
     case MQ_ENC_OPT_SPLITK_TILES: *value = e->splitk_tiles; break;
     case MQ_ENC_OPT_X6_PRESPLIT: *value = e->x6_presplit ? 1 : 0; break;
+    case MQ_ENC_OPT_ROWS_PLANES: *value = e->rows_planes ? 1 : 0; break;
     default: MQ_FAIL(MQ_EINVAL, "unknown encoder option %d", option);
   }
   return MQ_OK;

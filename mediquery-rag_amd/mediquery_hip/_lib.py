@@ -26,6 +26,7 @@ MQ_ENC_OPT_ROWS_MAX, MQ_ENC_OPT_ROWS_SPLITS, MQ_ENC_OPT_SPLITK_MAX = 0, 1, 2
 MQ_ENC_OPT_LN_ROWS_PER_WAVE, MQ_ENC_OPT_FUSE_ATTN_OPROJ, MQ_ENC_OPT_FUSED_LN = 3, 4, 5
 MQ_ENC_OPT_SPLITK_TILES, MQ_ENC_OPT_LN_ON_LOAD, MQ_ENC_OPT_RESIDENT_LAYERS = 6, 7, 8
 MQ_ENC_OPT_X6_PRESPLIT = 9
+MQ_ENC_OPT_ROWS_PLANES = 10
 
 
 class MQError(RuntimeError):

@@ -266,7 +266,8 @@ class Encoder:
                "splitk_max": _lib.MQ_ENC_OPT_SPLITK_MAX, "ln_rows_per_wave": _lib.MQ_ENC_OPT_LN_ROWS_PER_WAVE,
                "fuse_attn_oproj": _lib.MQ_ENC_OPT_FUSE_ATTN_OPROJ, "fused_ln": _lib.MQ_ENC_OPT_FUSED_LN,
                "splitk_tiles": _lib.MQ_ENC_OPT_SPLITK_TILES, "ln_on_load": _lib.MQ_ENC_OPT_LN_ON_LOAD,
-               "resident_layers": _lib.MQ_ENC_OPT_RESIDENT_LAYERS, "x6_presplit": _lib.MQ_ENC_OPT_X6_PRESPLIT}
+               "resident_layers": _lib.MQ_ENC_OPT_RESIDENT_LAYERS, "x6_presplit": _lib.MQ_ENC_OPT_X6_PRESPLIT,
+               "rows_planes": _lib.MQ_ENC_OPT_ROWS_PLANES}
 
     def set_option(self, name, value):
         """Tuning option of the forward (mq_encoder_set_option): rows_max, rows_splits,
@@ -275,7 +276,9 @@ class Encoder:
         index with the default cache policy and later layers non-temporally, so the first
         layers' weights stay in MALL between single queries; outputs are bit-identical),
         x6_presplit (split-f32 precision: 1, default, multiplies the weights' W3 plane images
-        split once at load; 0 = the tiles that re-split both operands; bit-identical)."""
+        split once at load; 0 = the tiles that re-split both operands; bit-identical),
+        rows_planes (few-row forward: 0, default, merges the two-addend hand-offs into one plane
+        by atomic adds; 1 = two planes; bit-identical)."""
         _lib.call("mq_encoder_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name):

@@ -312,3 +312,36 @@ def test_x6_presplit_bit_identical(require_gpu, B, L, layers, pool):
     assert np.array_equal(got, old), float(np.abs(got - old).max())
     ref = OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask)
     _close(got, ref)
+
+
+@pytest.mark.parametrize("B,L,layers,pool,gelu", [
+    (1, 32, 12, None, None),        # the single-query bench shape (frag16 Q/K/V^T, CLS-only last layer)
+    (1, 20, 3, POOL_MEAN, None),    # L % 16 != 0: row-major QKV for the fused attention
+    (2, 32, 2, None, GELU_TANH),    # two sequences, both 16-row aligned
+    (3, 21, 2, POOL_MEAN, None),    # ragged rows (63): the last 16-row block partly past M
+])
+def test_few_row_plane_merge_bit_identical(require_gpu, B, L, layers, pool, gelu):
+    """Few-row forward (r6): FFN-down's two K splits and the fused attention's two head
+    groups add into ONE zeroed plane by atomic adds (rows_planes = 0, default) - two addends
+    per element, so bitwise the p0 + p1 the consumer summed from two planes (rows_planes =
+    1) - run to run and against the oracle."""
+    kw = {"layers": layers}
+    if pool is not None:
+        kw["pooling"] = pool
+    if gelu is not None:
+        kw["gelu"] = gelu
+    cfg = BertConfig(**kw) if layers != 12 else DMETA_BASE
+    rng = np.random.default_rng(B * 13 + L)
+    ids = rng.integers(0, cfg.vocab_size, (B, L)).astype(np.int32)
+    mask = np.ones((B, L), np.int32)
+    if B > 1:
+        mask[0, int(rng.integers(1, L)):] = 0
+    enc = Encoder(cfg)
+    assert enc.get_option("rows_planes") == 0
+    got = enc.embed(ids, mask)
+    again = enc.embed(ids, mask)
+    enc.set_option("rows_planes", 1)
+    planes = enc.embed(ids, mask)
+    assert np.array_equal(got, again)
+    assert np.array_equal(got, planes), float(np.abs(got - planes).max())
+    _close(got, OracleEncoder(cfg, synthetic_state_dict(cfg, 0)).embed(ids, mask))
