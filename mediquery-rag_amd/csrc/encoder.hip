@@ -2316,7 +2316,9 @@ void launch_attn_oproj(int hg, bool qf, bool acc, int nkb, dim3 grid, hipStream_
     else if (acc) go(IC<6>{}, std::false_type{}, std::true_type{});
     else go(IC<6>{}, std::false_type{}, std::false_type{});
   } else {
-    if (qf) go(IC<4>{}, std::true_type{}, std::false_type{});
+    if (qf && acc) go(IC<4>{}, std::true_type{}, std::true_type{});
+    else if (qf) go(IC<4>{}, std::true_type{}, std::false_type{});
+    else if (acc) go(IC<4>{}, std::false_type{}, std::true_type{});
     else go(IC<4>{}, std::false_type{}, std::false_type{});
   }
 }
