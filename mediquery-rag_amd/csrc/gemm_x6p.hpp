@@ -31,21 +31,25 @@ inline size_t w3_row_offset(int64_t row0, int64_t K) { return (size_t)(row0 / 32
 // Region split of a persistent GEMM's tile walk: the tile grid cut into 8 regions, rx
 // column blocks x 8 / rx row blocks, one walked by the workgroups sharing blockIdx.x % 8
 // (one XCD under round-robin dispatch: speed only), so an XCD's weight column panels stay
-// in its L2 across rounds instead of every round re-reading them.  The pick: the rx with
-// the fewest per-XCD operand bytes (its A row panels + its W column panels), 0 (the plain
-// round-robin walk) when every workgroup has at most one tile.  r6, K2p at M = 8192: QKV
-// 152.8 -> 134.9 us (rx 4) / 138.4 (rx 2, the pick), the other shapes unchanged
-// (profiles/r6/ab_x6p_regions/).
+// in its L2 across rounds instead of every round re-reading them.  The pick models an XCD's
+// operand reads: its A row panels once, its W column panels once if they fit the 4 MB L2,
+// else once per round; 0 (the plain round-robin walk) when every workgroup has at most one
+// tile.  r6, K2p at M = 8192 (profiles/r6/ab_x6p_regions/): rx 4 for QKV (152.8 -> 134.9
+// us, FETCH 210 -> 181 MB) and FFN-up (time unchanged, FETCH 265 -> 205 MB).
 inline int region_pick_rx(int64_t tiles_m, int64_t tiles_n, double a_bytes_per_row_tile,
                           double w_bytes_per_col_tile, int64_t grid) {
   if (tiles_m * tiles_n <= grid || grid < 8) return 0;
+  const double l2 = 4.0 * 1024 * 1024;
+  const int64_t per_xcd = grid / 8;
   int best = 0;
   double best_b = 0;
   for (int rx = 1; rx <= 8; rx *= 2) {
     const int ry = 8 / rx;
     if (rx > tiles_n || ry > tiles_m) continue;
-    const double b = (double)((tiles_m + ry - 1) / ry) * a_bytes_per_row_tile +
-                     (double)((tiles_n + rx - 1) / rx) * w_bytes_per_col_tile;
+    const int64_t rm = (tiles_m + ry - 1) / ry, rn = (tiles_n + rx - 1) / rx;
+    const int64_t rounds = (rm * rn + per_xcd - 1) / per_xcd;
+    const double w = (double)rn * w_bytes_per_col_tile;
+    const double b = (double)rm * a_bytes_per_row_tile + (w <= l2 ? w : w * (double)rounds);
     if (best == 0 || b < best_b) {
       best = rx;
       best_b = b;
