@@ -38,6 +38,14 @@ namespace mq {
 // running max -> lmax[list][q]) and TS_APPEND (every block: score >= tau[q] appended to
 // the query's survivor list by one atomicAdd; rare by construction).
 constexpr int kTsWaves = 8;      // waves per workgroup (32 queries each)
+// Waves that issue the ring's DMAs.  4 = waves 0-3, one per SIMD: the other wave of every
+// SIMD runs its MFMA chain without DMA issues.  Measured (profiles/r6/k9t_dma_waves.txt, one
+// box, 1M rows): K9t append 453 us at 8 waves, 398 at 4, 543 at 2, 577 at 1 (B = 256).
+#ifndef MQ_TS_DMAW
+#define MQ_TS_DMAW 4
+#endif
+constexpr int kTsDmaWaves = MQ_TS_DMAW;
+static_assert(kTsDmaWaves == 8 || kTsDmaWaves == 4 || kTsDmaWaves == 2 || kTsDmaWaves == 1, "DMA waves");
 constexpr int kTsQ = kTsWaves * 32;  // queries per workgroup
 constexpr int kTsBufs = 3;       // LDS ring depth
 constexpr int kTsPeriod = 16;    // sample pass: every 16th block
@@ -88,8 +96,9 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   constexpr int ROW_B = NCH * 128;             // bf16 row bytes
   constexpr int BLK_B = kTsRows * ROW_B;       // one staged block (the shadow is padded to
                                                // whole blocks: no row clamping)
-  constexpr int DMA_PER_WAVE = NCH * 4 / kTsWaves;
-  static_assert(NCH % 2 == 0 && DMA_PER_WAVE * kTsWaves == NCH * 4, "8 waves share a block's DMAs");
+  constexpr int DMA_PER_WAVE = NCH * 4 / kTsDmaWaves;  // (waves past kTsDmaWaves issue none)
+  constexpr int DSTEP = NCH * 4 / DMA_PER_WAVE;         // chain steps between a wave's DMAs
+  static_assert(NCH % 2 == 0 && DMA_PER_WAVE * kTsDmaWaves == NCH * 4, "the DMA waves share a block's DMAs");
   // one LDS array: the row ring, then each wave's survivor list (TS_APPEND)
   constexpr int SURV_B = MODE == TS_APPEND ? kTsWaves * kTsWaveSurv * (int)sizeof(Survivor) : 0;
   __shared__ __attribute__((aligned(1024))) unsigned char ring[kTsBufs * BLK_B + SURV_B];
@@ -98,6 +107,7 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   const unsigned ring_lds = (unsigned)(uintptr_t)(lds_void_t*)ring;  // LDS byte address
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool dma_wave = wave < kTsDmaWaves;
   const int col = lane & 31, h = lane >> 5;
   const int qw0 = blockIdx.y * kTsQ + wave * 32;  // this wave's first query
   const int q = min(qw0 + col, nq - 1);           // lanes past nq compute a duplicate column
@@ -138,6 +148,7 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
            ring_lds + buf * BLK_B + d * 1024);
   };
   auto issue = [&](int i, int buf) __attribute__((always_inline)) {
+    if (!dma_wave) return;
 #pragma unroll
     for (int tt = 0; tt < DMA_PER_WAVE; ++tt) issue_one(i, buf, tt);
   };
@@ -171,8 +182,8 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     // Hand-scheduled chain: fragment reads run three MFMA steps ahead (the compiler's own
     // order reads one step ahead and waits out the LDS latency before every other MFMA),
-    // and block i+2's DMAs are spread over the chain, one every 8 steps, instead of
-    // delaying its start.
+    // and block i+2's DMAs (DMA waves only) are spread over the chain, one every DSTEP
+    // steps, instead of delaying its start.
     bf16x8 a[4];
     auto frag = [&](int st) __attribute__((always_inline)) {
       const int c = st >> 2, s = st & 3;
@@ -186,9 +197,11 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
     const unsigned nlds = ring_lds + ((i + 2) % kTsBufs) * BLK_B;
     static_for<NCH * 4>([&](auto sc) {
       constexpr int st = decltype(sc)::value;
-      if constexpr (st % 8 == 0 && st / 8 < DMA_PER_WAVE && !(MQ_TS_DBG & 2)) {
-        const int d = wave * DMA_PER_WAVE + st / 8;
-        glds16(nsrc, dofs[d & 1] + (unsigned)((d & 3) * 8 * ROW_B + (d >> 2) * 128), nlds + d * 1024);
+      if constexpr (st % DSTEP == 0 && st / DSTEP < DMA_PER_WAVE && !(MQ_TS_DBG & 2)) {
+        if (dma_wave) {
+          const int d = wave * DMA_PER_WAVE + st / DSTEP;
+          glds16(nsrc, dofs[d & 1] + (unsigned)((d & 3) * 8 * ROW_B + (d >> 2) * 128), nlds + d * 1024);
+        }
       }
       if constexpr (st + 3 < NCH * 4) a[(st + 3) & 3] = (MQ_TS_DBG & 4) ? qf[(st + 5) % (NCH * 4)] : frag(st + 3);
       __builtin_amdgcn_sched_barrier(0);
