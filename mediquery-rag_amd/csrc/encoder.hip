@@ -1254,6 +1254,8 @@ void launch_attention(int B, int L, int heads, int qt, int H, float scale, const
                       const int* mask, float* ctx, hipStream_t s) {
   const int triples = B * heads * qt, key_tiles = (L + 31) / 32;
   const dim3 grid(triples);
+  // (6 or 4 heads per workgroup, 2-3 workgroups per CU: 0.386 / 0.337 vs 0.305 ms per step,
+  // same box, r6)
   if (key_tiles == 1 && heads == 12 && triples >= 12 * 256)  // BERT-base batches: 12 heads per workgroup
     hipLaunchKernelGGL((attention_kernel<1, 12>), dim3(B * qt), dim3(768), 0, s, qkv, mask, L, H, heads, qt, scale,
                        ctx);
