@@ -67,6 +67,9 @@ typedef struct mq_encoder mq_encoder;
 const char* mq_last_error(void);
 /* Library build string (arch, version). */
 const char* mq_version(void);
+/* Build provenance: the first 16 hex digits of the SHA-256 of the csrc/ sources, the
+ * Makefile and this header the library was built from (csrc/Makefile STAMPED). */
+const char* mq_build_source_hash(void);
 /* Number of visible HIP devices (0 without a GPU); never fails. */
 int mq_device_count(void);
 

@@ -5,6 +5,7 @@ The library is built in-tree by `make -C mediquery-rag_amd/csrc` (or
 or fails to load, importing the product classes raises immediately.
 """
 import ctypes
+import hashlib
 import os
 
 try:  # load torch's HIP runtime first so the process has exactly one libamdhip64
@@ -58,6 +59,7 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 SIGNATURES = {
     "mq_last_error": (ctypes.c_char_p, []),
     "mq_version": (ctypes.c_char_p, []),
+    "mq_build_source_hash": (ctypes.c_char_p, []),
     "mq_device_count": (_I, []),
     "mq_index_create": (_I, [_I, _I, _I64, _I, _PP]),
     "mq_index_destroy": (_I, [_P]),
@@ -147,6 +149,39 @@ def check(fn_name, rc):
 
 def call(fn_name, *args):
     return check(fn_name, getattr(lib(), fn_name)(*args))
+
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+_STAMPED_EXT = (".hip", ".cpp", ".hpp", ".inc")
+
+
+def tree_source_hash(csrc=CSRC):
+    """csrc/Makefile's STAMPED hash recomputed from the sources beside the package: the
+    sorted csrc/*.hip *.cpp *.hpp *.inc, then the Makefile, then include/mq.h."""
+    names = sorted(f for f in os.listdir(csrc) if f.endswith(_STAMPED_EXT))
+    paths = [os.path.join(csrc, f) for f in names]
+    paths += [os.path.join(csrc, "Makefile"), os.path.join(csrc, "..", "..", "include", "mq.h")]
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_source_hash():
+    """The source hash the loaded library was built from (mq_build_source_hash)."""
+    return lib().mq_build_source_hash().decode()
+
+
+def check_build_fresh():
+    """Raise if the loaded library was not built from the sources in this tree (a stale
+    prebuilt .so); a no-op when the sources are absent (an installed package)."""
+    if not os.path.isdir(CSRC):
+        return
+    built, tree = built_source_hash(), tree_source_hash()
+    if built != tree:
+        raise ImportError("libmqhip.so at %s was built from sources %s, the tree holds %s: "
+                          "rebuild with `make -C mediquery-rag_amd/csrc`" % (LIB_PATH, built, tree))
 
 
 def device_count():

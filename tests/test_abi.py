@@ -34,6 +34,15 @@ def test_version_and_device_count():
     assert _lib.device_count() >= 0
 
 
+def test_library_built_from_this_tree():
+    """The .so carries the hash of the sources it was compiled from (csrc/Makefile
+    STAMPED); it equals the tree's, so the library the GPU runs is not a stale prebuilt."""
+    built = _lib.built_source_hash()
+    assert len(built) == 16 and int(built, 16) >= 0
+    assert built == _lib.tree_source_hash()
+    _lib.check_build_fresh()
+
+
 def test_weight_count_matches_python_layout():
     for cfg in (DMETA_BASE, BertConfig(layers=2)):
         c = _lib.BertConfigC.from_config(cfg)

@@ -202,8 +202,9 @@ def test_upsert_by_existing_id_replaces_row_and_persists(embeddings, docs, tmp_p
 
 
 def test_filtered_search_equals_oracle_on_allowed_rows(embeddings, docs):
-    """filter= scores only the allowed rows (vectorised where, device gather into one
-    reused scratch index): the result equals the exact top-k over the rows _match admits,
+    """filter= scores only the allowed rows (the where-mask built on the device from the
+    metadata code columns, then one masked search - the masked scan, or at this store size
+    the masked row gather): the result equals the exact top-k over the rows _match admits,
     for several filters in a row and for a repeated one."""
     from mediquery_hip.vectorstore import _match
     store = HipChroma.from_documents(documents=docs, embedding=embeddings)
