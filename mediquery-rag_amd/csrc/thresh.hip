@@ -49,6 +49,10 @@ static_assert(kTsDmaWaves == 8 || kTsDmaWaves == 4 || kTsDmaWaves == 2 || kTsDma
 constexpr int kTsQ = kTsWaves * 32;  // queries per workgroup
 constexpr int kTsBufs = 3;       // LDS ring depth
 constexpr int kTsPeriod = 16;    // sample pass: every 16th block
+#ifndef MQ_TS_BF_PERIOD
+#define MQ_TS_BF_PERIOD 16
+#endif
+constexpr int kTsBfPeriod = MQ_TS_BF_PERIOD;  // ... of the bf16 scan
 
 enum { TS_MAX = 0, TS_APPEND = 1 };
 
@@ -313,6 +317,14 @@ __global__ __launch_bounds__(256) void bf16_tau_kernel(const float* __restrict__
 // re-run one tier down).  With `fail` set (the approximate bf16 mode, no certificate), a
 // query with more than kTsCap or fewer than kc survivors is appended to fail[] instead,
 // for the caller to re-run on the tiled scan.
+//
+// Past 256 survivors (a block-uniform branch) ranks are counted only among the survivors
+// that can still place: T = the kc-th best of the 256 threads' own best survivors bounds
+// the kc-th best overall from below (the thread maxima are distinct survivors), so every
+// survivor worse than T has rank >= kc, and every survivor better than one at or above T
+// is at or above T too - ranks counted in the filtered set are the exact ranks (the same
+// output as counting over all survivors, at O(n + 256^2 + m^2) instead of O(n^2): a query
+// with thousands of survivors held the whole launch for 30-500 us).
 __global__ __launch_bounds__(256) void bf16_select_kernel(const float* __restrict__ cs,
                                                           const int* __restrict__ ci,
                                                           const int* __restrict__ count,
@@ -321,27 +333,79 @@ __global__ __launch_bounds__(256) void bf16_select_kernel(const float* __restric
                                                           int64_t* __restrict__ out_i,
                                                           int* __restrict__ fail_count,
                                                           int64_t* __restrict__ fail) {
-  __shared__ float ls[kTsCap];
-  __shared__ int li[kTsCap];
+  __shared__ float ls[kTsCap], fs[kTsCap], ts[256];
+  __shared__ int li[kTsCap], fi[kTsCap], ti[256];
+  __shared__ float cut_s;
+  __shared__ int cut_i, nf;
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
   const int total = count[q];
   if (fail && tid == 0 && (total > kTsCap || total < kc)) fail[atomicAdd(fail_count, 1)] = q;
   const int cnt = min(total, kTsCap);
+  float bs = -INFINITY;
+  int bi = -1;  // no survivor (as unsigned: after every real id)
   for (int i = tid; i < cnt; i += 256) {
-    ls[i] = cs[q * kTsCap + i];
-    li[i] = ci[q * kTsCap + i];
-  }
-  __syncthreads();
-  for (int i = tid; i < cnt; i += 256) {
-    const float x = ls[i];
-    const int xi = li[i];
-    int rank = 0;
-    for (int j = 0; j < cnt; ++j) rank += better(ls[j], li[j], x, xi) ? 1 : 0;
-    if (rank < kc) {
-      out_s[q * kc + rank] = rank == kc - 1 && total > kTsCap ? INFINITY : x;
-      out_i[q * kc + rank] = xi;
+    const float x = cs[q * kTsCap + i];
+    const int xi = ci[q * kTsCap + i];
+    ls[i] = x;
+    li[i] = xi;
+    if (bi == -1 || better(x, (unsigned)xi, bs, (unsigned)bi)) {
+      bs = x;
+      bi = xi;
     }
+  }
+  // exact rank of each of the m survivors in (rs, ri) among them; the top kc go out
+  auto rank_out = [&](const float* rs, const int* ri, int m) __attribute__((always_inline)) {
+    for (int i = tid; i < m; i += 256) {
+      const float x = rs[i];
+      const int xi = ri[i];
+      int rank = 0;
+      for (int j = 0; j < m; ++j) rank += better(rs[j], (unsigned)ri[j], x, (unsigned)xi) ? 1 : 0;
+      if (rank < kc) {
+        out_s[q * kc + rank] = rank == kc - 1 && total > kTsCap ? INFINITY : x;
+        out_i[q * kc + rank] = xi;
+      }
+    }
+  };
+  if (cnt <= 256) {
+    __syncthreads();
+    rank_out(ls, li, cnt);
+  } else {
+    ts[tid] = bs;
+    ti[tid] = bi;
+    if (tid == 0) {
+      cut_s = -INFINITY;  // (kc > 256: no cut)
+      cut_i = -1;
+      nf = 0;
+    }
+    __syncthreads();
+    int rank = 0;  // every thread holds a survivor here
+    for (int j = 0; j < 256; ++j) rank += better(ts[j], (unsigned)ti[j], bs, (unsigned)bi) ? 1 : 0;
+    if (rank == kc - 1) {
+      cut_s = bs;
+      cut_i = bi;
+    }
+    __syncthreads();
+    const float Ts = cut_s;
+    const unsigned Ti = (unsigned)cut_i;
+    // the survivors at or above T to fs / fi: a ballot and lane prefix per wave, one LDS
+    // slot claim per wave and round
+    const int lane = tid & 63;
+    for (int base = 0; base < cnt; base += 256) {
+      const int i = base + tid;
+      const bool keep = i < cnt && !better(Ts, Ti, ls[i], (unsigned)li[i]);
+      const unsigned long long bal = __ballot(keep);
+      int slot0 = 0;
+      if (lane == 0 && bal) slot0 = atomicAdd(&nf, __popcll(bal));
+      slot0 = __shfl(slot0, 0);
+      if (keep) {
+        const int slot = slot0 + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+        fs[slot] = ls[i];
+        fi[slot] = li[i];
+      }
+    }
+    __syncthreads();
+    rank_out(fs, fi, nf);
   }
   for (int i = cnt + tid; i < kc; i += 256) {  // (never on overflow: kTsCap > kc)
     out_s[q * kc + i] = tau[q];
@@ -361,7 +425,7 @@ void launch_nch(const ThreshArgs& a, hipStream_t s, Timeline* tl) {
   const uint4* qb = reinterpret_cast<const uint4*>(a.q16);
   tl->mark(s, 0);
   hipLaunchKernelGGL((bf16_thresh_kernel<NCH, TS_MAX, MASKED>), dim3(G, gy), dim3(512), 0, s, qb, a.nq, a.rows,
-                     a.n, n_blocks, kTsPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.mask);
+                     a.n, n_blocks, kTsBfPeriod, a.tau, a.lmax, a.count, a.cs, a.ci, a.mask);
   tl->mark(s, 1);
   hipLaunchKernelGGL(bf16_tau_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a.lmax, 2 * G, a.nq,
                      a.tau_rank, a.tau, a.count);
