@@ -116,7 +116,7 @@ def mean(v):
 
 # the exact-f32 encoder GEMM (X6 = false, BF16 = false, optional slice-depth parameter)
 # followed by its epilogue id
-EXACT_GEMM = r"gemm_nt_kernel<mq::F32Tile<\d+, \d+, \d+, \d+, false, \d+, false(, \d+)?>, "
+EXACT_GEMM = r"gemm_nt_kernel<mq::F32Tile<\d+, \d+, \d+, \d+, false, \d+, false(, \d+)?(, (true|false))?>, "
 # the split-f32 GEMM on pre-split weights (gemm_x6p.hip), its epilogue id captured
 X6P_GEMM = r"gemm_x6p_kernel<mq::X6pTile<[^>]*>, (\d)>"
 # ... then gemm_nt_kernel's LN_IN argument (r4: LayerNorm on load, false by default)
@@ -127,8 +127,8 @@ CLASSES = {
     "flat_search_kernel": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, false(, \d+)?>, \d+>",
     "flat_search_kernel_x6": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, true, \d, false(, \d+)?>, 8>",
     "flat_search_kernel_bf16": r"flat_search_kernel<mq::F32Tile<2, 2, 2, 2, false, \d, true(, \d+)?>, 8>",
-    "bf16_thresh_kernel": r"bf16_thresh_kernel<\d+, 1>",
-    "bf16_thresh_sample": r"bf16_thresh_kernel<\d+, 0>",
+    "bf16_thresh_kernel": r"bf16_thresh_kernel<\d+, 1(, false)?>",  # (unmasked)
+    "bf16_thresh_sample": r"bf16_thresh_kernel<\d+, 0(, false)?>",
     "i8_thresh_kernel": r"i8_thresh_kernel<\d, 1, 1>",
     "i8_thresh_sample": r"i8_thresh_kernel<\d, 1, 0>",
     "qkv_gemm": r"gemm_nt_kernel<mq::F32Tile<\d, \d, \d, \d, false, \d, false>, 0>",
