@@ -849,6 +849,14 @@ def main():
                                        "fp32 accumulate) for the encoder and the direct scan"),
     }
     out["distributed"] = dist_info
+    # which library ran: the source hash compiled into it, and whether it is this tree's
+    built = _lib.built_source_hash()
+    try:
+        tree = _lib.tree_source_hash()
+    except OSError:
+        tree = None
+    out["library"] = {"path": os.path.relpath(_lib.LIB_PATH, ROOT), "source_hash": built,
+                      "built_from_this_tree": built == tree if tree else None}
     out["config4_sharded"] = c4
     out["config5_bf16_rerank"] = cfg5
     out["secondary_long_queries"] = sec
