@@ -133,6 +133,7 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   for (int i = 0; i < NCH * 4; ++i) asm volatile("" : "+v"(qf[i]));
   asm volatile("" : "+v"(t));
 
+  const int n_rows_i = (int)min(n_rows, (int64_t)INT_MAX);
   // this workgroup's blocks: j_i = (blockIdx.x + i * gridDim.x) * period
   const int64_t stride = (int64_t)gridDim.x * period;
   const int64_t first = (int64_t)blockIdx.x * period;
@@ -167,11 +168,16 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
   }
   const bool active = qw0 < nq;
   for (int i = 0; i < nb; ++i) {
-    unsigned mw = ~0u;  // (MASKED) block i's row bits
-    if constexpr (MASKED) {
+    // (MASKED) block i's row bits: a scalar load, here for the sample pass; the append
+    // pass loads them in its rare survivor path only
+    auto mask_word = [&]() __attribute__((always_inline)) {
+      unsigned w;
       const unsigned* mp = mask + (first + (int64_t)i * stride);
-      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(mw) : "s"(mp) : "memory");
-    }
+      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(mp) : "memory");
+      return w;
+    };
+    unsigned mw = ~0u;
+    if constexpr (MASKED && MODE == TS_MAX) mw = mask_word();
     // own DMAs of block i landed (block i+1's may still fly), then everyone's, and every
     // wave is done reading block i-1, whose buffer this iteration refills
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_PER_WAVE) : "memory");
@@ -214,12 +220,23 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
     });
     const int64_t row0 = (first + (int64_t)i * stride) * kTsRows;
     const bool full = row0 + kTsRows <= n_rows;
+    if constexpr (MASKED && MODE == TS_MAX) {
+      // rows outside the mask score -inf, in place.  The lane's mask word and the fill
+      // value are made here, by asm the compiler cannot hoist above the chain, where
+      // every VGPR is taken (acc element e is row (e & 3) + 8 (e >> 2) + 4 h)
+      unsigned mwl;
+      float off;
+      asm volatile("v_lshrrev_b32 %0, %1, %2" : "=v"(mwl) : "v"(4 * h), "s"(mw));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(off) : "i"(0xff800000u));
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (!((mwl >> ((e & 3) + 8 * (e >> 2))) & 1u)) acc[e] = off;
+    }
     if constexpr (MODE == TS_MAX) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t row = row0 + acc_row(0, e, lane);
-        const bool here = !MASKED || ((mw >> acc_row(0, e, lane)) & 1u);
-        if ((full || row < n_rows) && here) mx = fmaxf(mx, acc[e]);
+        if (full || row < n_rows) mx = fmaxf(mx, acc[e]);
       }
     } else {
       // survivors go to this wave's LDS list (a ballot + lane prefix picks the slots);
@@ -227,24 +244,30 @@ __global__ __launch_bounds__(512, 2) void bf16_thresh_kernel(
       // vmcnt(0) would drain the ring - ever runs inside it
       bool any = false;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) any |= acc[e] >= t && (!MASKED || ((mw >> acc_row(0, e, lane)) & 1u));
+      for (int e = 0; e < 16; ++e) any |= acc[e] >= t;
       if (__builtin_amdgcn_ballot_w64(any && qvalid)) {  // rare: ~128 survivors per query
+        // (MASKED: the lane's mask word, by asm so that it is not hoisted out of the loop)
+        unsigned mwl = 0;
+        if constexpr (MASKED) asm volatile("v_lshrrev_b32 %0, %1, %2" : "=v"(mwl) : "v"(4 * h), "s"(mask_word()));
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int64_t row = row0 + acc_row(0, e, lane);
-          const bool hit = acc[e] >= t && row < n_rows && qvalid &&
-                           (!MASKED || ((mw >> acc_row(0, e, lane)) & 1u));
+          const int row = (int)row0 + acc_row(0, e, lane);  // (ids are 32-bit: Survivor, ci)
+          // (MASKED: the mask is applied here only - a masked row that clears tau enters
+          // this rare path and is dropped; any mask term in the every-block test above cost
+          // the append kernel a spilled query fragment, reloaded per block)
+          const bool hit = acc[e] >= t && row < n_rows_i && qvalid &&
+                           (!MASKED || ((mwl >> ((e & 3) + 8 * (e >> 2))) & 1u));
           const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
           if (m) {
             const int pos = n_surv + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
             if (hit) {
               if (pos < kTsWaveSurv) {
-                surv[pos] = Survivor{acc[e], (int)row, q};
+                surv[pos] = Survivor{acc[e], row, q};
               } else {  // list full: straight to global (drains the ring; rarer still)
                 const int slot = atomicAdd(count + q, 1);
                 if (slot < kTsCap) {
                   cs[(int64_t)q * kTsCap + slot] = acc[e];
-                  ci[(int64_t)q * kTsCap + slot] = (int)row;
+                  ci[(int64_t)q * kTsCap + slot] = row;
                 }
               }
             }
